@@ -1,0 +1,64 @@
+"""Build libqdec_hip.so in-tree with hipcc for gfx950.
+
+``python -m exp_ldpc_amd.build`` (also called by ``__graft_entry__.build()``).
+The library is built here (hipcc cross-compiles without a GPU) and travels to the
+GPU box with the repository snapshot.
+
+Numerics flags: ``-ffp-contract=off`` (no fused multiply-add: every operation is
+rounded like the CPU oracle and ldpc's loops), IEEE fp32 division, fp32
+denormals kept.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libqdec_hip.so")
+SOURCES = ["qdec_abi.cpp", "qdec_bp.hip", "qdec_sample.hip"]
+HEADERS = ["qdec_internal.h", os.path.join("..", "..", "include", "qdec.h")]
+ARCH = os.environ.get("QDEC_OFFLOAD_ARCH", "gfx950")
+
+FLAGS = [
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+    "-Wall", "-Wno-unused-result",
+]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: cannot build libqdec_hip.so")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-6000:]}")
+    if verbose and res.stderr:
+        print(res.stderr[-4000:], file=sys.stderr)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

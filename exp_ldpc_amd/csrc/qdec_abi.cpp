@@ -1,0 +1,479 @@
+// qdec_abi.cpp -- extern "C" entry points of libqdec_hip.so (include/qdec.h).
+//
+// Host-side graph preparation: CSR -> per-lane slot tables for the wave
+// kernels, flip-set tables for SSF, bit-packed logicals, priors in both
+// precisions; device upload; launches.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/qdec.h"
+#include "qdec_internal.h"
+
+using namespace qdec;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Fail : std::runtime_error {
+    int code;
+    Fail(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw Fail(-100 - (int)e, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return 0;
+    } catch (const Fail& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return -99;
+    } catch (...) {
+        g_last_error = "unknown error";
+        return -99;
+    }
+}
+
+// A device allocation list owned by the graph.
+struct DevArena {
+    std::vector<void*> ptrs;
+    template <typename T>
+    const T* upload(const std::vector<T>& h) {
+        void* d = nullptr;
+        const size_t bytes = std::max<size_t>(h.size() * sizeof(T), 16);
+        hip_check(hipMalloc(&d, bytes), "hipMalloc");
+        ptrs.push_back(d);
+        if (!h.empty()) hip_check(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy H2D");
+        return static_cast<const T*>(d);
+    }
+    void release() {
+        for (void* p : ptrs) (void)hipFree(p);
+        ptrs.clear();
+    }
+};
+
+}  // namespace
+
+struct qd_graph {
+    int device = 0;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    DevGraph dg{};
+    bool has_priors = false;
+    // host copies needed to rebuild tables
+    std::vector<int32_t> row_ptr, col_idx;
+    std::vector<int32_t> col_ptr, col_rows;  // CSC (row ids, ascending)
+    DevArena arena;                          // graph tables
+    DevArena flip_arena, lz_arena, prior_arena;
+    // workspace for the host-buffer API (grow only)
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+};
+
+namespace {
+
+template <typename T>
+int drs() { return lds_stride<T, kDR>(); }
+template <typename T>
+int dcs() { return lds_stride<T, kDC>(); }
+
+void set_device(qd_graph* g) { hip_check(hipSetDevice(g->device), "hipSetDevice"); }
+
+void build_tables(qd_graph* G, int m, int n) {
+    DevGraph& g = G->dg;
+    g.m = m;
+    g.n = n;
+    g.m_pad = std::max(64, (m + 63) / 64 * 64);
+    g.n_pad = std::max(64, (n + 63) / 64 * 64);
+    const auto& rp = G->row_ptr;
+    const auto& ci = G->col_idx;
+    const int E = rp[m];
+    // CSC with ascending rows; position of each edge inside its column list
+    G->col_ptr.assign(n + 1, 0);
+    for (int e = 0; e < E; ++e) G->col_ptr[ci[e] + 1]++;
+    for (int j = 0; j < n; ++j) G->col_ptr[j + 1] += G->col_ptr[j];
+    G->col_rows.assign(std::max(E, 1), 0);
+    std::vector<int> fill(G->col_ptr.begin(), G->col_ptr.end() - 1);
+    std::vector<int> edge_cpos(std::max(E, 1), 0);
+    for (int i = 0; i < m; ++i)
+        for (int e = rp[i]; e < rp[i + 1]; ++e) {
+            const int j = ci[e];
+            edge_cpos[e] = fill[j] - G->col_ptr[j];
+            G->col_rows[fill[j]++] = i;
+        }
+    g.max_rdeg = 0;
+    for (int i = 0; i < m; ++i) g.max_rdeg = std::max(g.max_rdeg, rp[i + 1] - rp[i]);
+    g.max_cdeg = 0;
+    for (int j = 0; j < n; ++j) g.max_cdeg = std::max(g.max_cdeg, G->col_ptr[j + 1] - G->col_ptr[j]);
+    if (g.max_rdeg > kDR || g.max_cdeg > kDC)
+        throw Fail(-20, "graph degrees exceed this build's wave kernel (check degree <= 8, variable degree <= 4)");
+    if (g.m_pad / 64 > 4 || g.n_pad / 64 > 9)
+        throw Fail(-21, "graph too large for this build's wave kernel (m <= 256, n <= 576)");
+
+    std::vector<uint8_t> r_deg(g.m_pad, 0), c_deg(g.n_pad, 0);
+    std::vector<uint16_t> r_col((size_t)kDR * g.m_pad, (uint16_t)g.n_pad);
+    std::vector<uint16_t> r_cslot[2], c_rslot[2];
+    const int DRS[2] = {drs<double>(), drs<float>()};
+    const int DCS[2] = {dcs<double>(), dcs<float>()};
+    for (int p = 0; p < 2; ++p) {
+        r_cslot[p].assign((size_t)kDR * g.m_pad, 0);
+        c_rslot[p].assign((size_t)kDC * g.n_pad, 0);
+        if ((size_t)g.m_pad * DRS[p] > 65535 || (size_t)g.n_pad * DCS[p] > 65535)
+            throw Fail(-21, "graph too large for 16-bit LDS slots");
+    }
+    for (int i = 0; i < m; ++i) {
+        r_deg[i] = (uint8_t)(rp[i + 1] - rp[i]);
+        for (int e = rp[i], k = 0; e < rp[i + 1]; ++e, ++k) {
+            const int j = ci[e];
+            r_col[(size_t)k * g.m_pad + i] = (uint16_t)j;
+            for (int p = 0; p < 2; ++p) {
+                r_cslot[p][(size_t)k * g.m_pad + i] = (uint16_t)(j * DCS[p] + edge_cpos[e]);
+            }
+        }
+    }
+    for (int j = 0; j < n; ++j) {
+        c_deg[j] = (uint8_t)(G->col_ptr[j + 1] - G->col_ptr[j]);
+        for (int t = G->col_ptr[j], k = 0; t < G->col_ptr[j + 1]; ++t, ++k) {
+            const int i = G->col_rows[t];
+            // position of this edge inside row i
+            int kr = 0;
+            for (int e = rp[i]; e < rp[i + 1]; ++e, ++kr)
+                if (ci[e] == j) break;
+            for (int p = 0; p < 2; ++p) c_rslot[p][(size_t)k * g.n_pad + j] = (uint16_t)(i * DRS[p] + kr);
+        }
+    }
+    g.r_deg = G->arena.upload(r_deg);
+    g.r_col = G->arena.upload(r_col);
+    g.c_deg = G->arena.upload(c_deg);
+    for (int p = 0; p < 2; ++p) {
+        g.slots[p].r_cslot = G->arena.upload(r_cslot[p]);
+        g.slots[p].c_rslot = G->arena.upload(c_rslot[p]);
+    }
+    g.row_ptr = G->arena.upload(G->row_ptr);
+    g.col_idx = G->arena.upload(G->col_idx);
+}
+
+void check_graph(const qd_graph* g) {
+    if (!g) throw Fail(-1, "null graph handle");
+}
+
+void check_params(const qd_graph* g, const qd_params* p) {
+    if (!p) throw Fail(-2, "null params");
+    if (p->method != QD_MIN_SUM && p->method != QD_PRODUCT_SUM) throw Fail(-3, "unknown BP method");
+    if (p->precision != QD_F32 && p->precision != QD_F64) throw Fail(-4, "unknown precision");
+    if (!g->has_priors) throw Fail(-5, "priors not set (qd_graph_set_priors)");
+    if (p->ssf && g->dg.n_gen <= 0) throw Fail(-6, "SSF requested but the graph has no flip sets");
+}
+
+DecodeArgs make_args(const qd_graph* g, const qd_params* p, int64_t B, const uint8_t* syn, const uint8_t* base,
+                     const uint8_t* readout, uint8_t* x_out, uint8_t* corr_out, void* llr_out, int32_t* iters,
+                     uint8_t* status, int32_t* ssf_steps, uint8_t* fail) {
+    DecodeArgs a{};
+    a.B = B;
+    a.max_iter = p->max_iter > 0 ? p->max_iter : g->dg.n;
+    a.ssf = p->ssf ? 1 : 0;
+    a.ssf_max_steps = p->ssf_max_steps;
+    a.syn_flags = p->syn_flags & 3;
+    a.ms_scaling = p->ms_scaling;
+    a.syn = syn;
+    a.base = base;
+    a.readout = readout;
+    a.x_out = x_out;
+    a.corr_out = corr_out;
+    a.llr_out = llr_out;
+    a.iters = iters;
+    a.status = status;
+    a.ssf_steps = ssf_steps;
+    a.fail = fail;
+    if (!syn && !(a.syn_flags && (base || readout))) throw Fail(-7, "no syndrome source");
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qd_abi_version(void) { return QDEC_ABI_VERSION; }
+
+const char* qd_last_error(void) { return g_last_error.c_str(); }
+
+int qd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx, int32_t n_data,
+                    int32_t fold_blocks, int32_t device, qd_graph** out) {
+    return guarded([&] {
+        if (!out) throw Fail(-1, "null output handle");
+        *out = nullptr;
+        if (m <= 0 || n <= 0 || !row_ptr || !col_idx) throw Fail(-10, "invalid graph shape or null arrays");
+        if (n_data <= 0 || fold_blocks <= 0 || (int64_t)n_data * fold_blocks > n)
+            throw Fail(-11, "invalid fold (n_data * fold_blocks must be <= n)");
+        if (row_ptr[0] != 0) throw Fail(-12, "row_ptr[0] must be 0");
+        for (int i = 0; i < m; ++i) {
+            if (row_ptr[i + 1] < row_ptr[i]) throw Fail(-12, "row_ptr not monotone");
+            for (int e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+                if (col_idx[e] < 0 || col_idx[e] >= n) throw Fail(-13, "column index out of range");
+                if (e > row_ptr[i] && col_idx[e] <= col_idx[e - 1])
+                    throw Fail(-14, "column indices must be strictly ascending within a row");
+            }
+        }
+        int ndev = 0;
+        hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+        if (device < 0 || device >= ndev) throw Fail(-15, "device ordinal out of range");
+        auto* G = new qd_graph();
+        try {
+            G->device = device;
+            set_device(G);
+            hipDeviceProp_t prop;
+            hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+            G->num_cus = prop.multiProcessorCount;
+            hip_check(hipStreamCreateWithFlags(&G->stream, hipStreamNonBlocking), "hipStreamCreate");
+            G->row_ptr.assign(row_ptr, row_ptr + m + 1);
+            G->col_idx.assign(col_idx, col_idx + row_ptr[m]);
+            G->dg.n_data = n_data;
+            G->dg.fold_blocks = fold_blocks;
+            build_tables(G, m, n);
+            G->dg.lz_words = (n_data + 63) / 64;
+            G->dg.k = 0;
+            G->dg.lz = nullptr;
+            G->dg.n_gen = 0;
+        } catch (...) {
+            G->arena.release();
+            if (G->stream) (void)hipStreamDestroy(G->stream);
+            delete G;
+            throw;
+        }
+        *out = G;
+    });
+}
+
+int qd_graph_destroy(qd_graph* g) {
+    return guarded([&] {
+        if (!g) return;
+        (void)hipSetDevice(g->device);
+        if (g->stream) (void)hipStreamSynchronize(g->stream);
+        g->arena.release();
+        g->flip_arena.release();
+        g->lz_arena.release();
+        g->prior_arena.release();
+        if (g->ws) (void)hipFree(g->ws);
+        if (g->stream) (void)hipStreamDestroy(g->stream);
+        delete g;
+    });
+}
+
+int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, const int32_t* gen_idx) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        if (n_gen <= 0 || !gen_ptr || !gen_idx) throw Fail(-30, "invalid flip sets");
+        DevGraph& g = G->dg;
+        const int gp = (n_gen + 63) / 64 * 64;
+        std::vector<uint8_t> w(gp, 0), nlc(gp, 0);
+        std::vector<uint16_t> q((size_t)kGenW * gp, 0), lc((size_t)kGenLC * gp, 0);
+        std::vector<uint32_t> qm((size_t)kGenW * gp, 0);
+        int wmax = 0;
+        for (int gi = 0; gi < n_gen; ++gi) {
+            const int a = gen_ptr[gi], b = gen_ptr[gi + 1];
+            if (b < a) throw Fail(-31, "gen_ptr not monotone");
+            const int wg = b - a;
+            if (wg > kGenW) throw Fail(-32, "flip-set generator weight exceeds 8");
+            std::vector<int> checks;
+            for (int k = 0; k < wg; ++k) {
+                const int qq = gen_idx[a + k];
+                if (qq < 0 || qq >= g.n) throw Fail(-33, "flip-set qubit out of range");
+                if (k > 0 && qq <= gen_idx[a + k - 1]) throw Fail(-34, "flip-set qubits must be strictly ascending");
+                for (int t = G->col_ptr[qq]; t < G->col_ptr[qq + 1]; ++t) checks.push_back(G->col_rows[t]);
+            }
+            std::sort(checks.begin(), checks.end());
+            checks.erase(std::unique(checks.begin(), checks.end()), checks.end());
+            if ((int)checks.size() > kGenLC) throw Fail(-35, "flip-set generator touches more than 32 checks");
+            w[gi] = (uint8_t)wg;
+            nlc[gi] = (uint8_t)checks.size();
+            wmax = std::max(wmax, wg);
+            for (size_t c = 0; c < checks.size(); ++c) lc[c * gp + gi] = (uint16_t)checks[c];
+            for (int k = 0; k < wg; ++k) {
+                const int qq = gen_idx[a + k];
+                q[(size_t)k * gp + gi] = (uint16_t)qq;
+                uint32_t mask = 0;
+                for (int t = G->col_ptr[qq]; t < G->col_ptr[qq + 1]; ++t) {
+                    const int c = (int)(std::lower_bound(checks.begin(), checks.end(), G->col_rows[t]) - checks.begin());
+                    mask ^= 1u << c;
+                }
+                qm[(size_t)k * gp + gi] = mask;
+            }
+        }
+        G->flip_arena.release();
+        g.g_w = G->flip_arena.upload(w);
+        g.g_nlc = G->flip_arena.upload(nlc);
+        g.g_q = G->flip_arena.upload(q);
+        g.g_lc = G->flip_arena.upload(lc);
+        g.g_qmask = G->flip_arena.upload(qm);
+        g.n_gen = n_gen;
+        g.g_pad = gp;
+        g.g_wmax = wmax;
+    });
+}
+
+int qd_graph_set_logicals(qd_graph* G, int32_t k, const uint8_t* lz) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        DevGraph& g = G->dg;
+        if (k < 0 || (k > 0 && !lz)) throw Fail(-40, "invalid logicals");
+        if (k > 256) throw Fail(-41, "more than 256 logicals not supported by this build");
+        const int W = g.lz_words;
+        std::vector<uint64_t> packed((size_t)std::max(k, 1) * W, 0);
+        for (int r = 0; r < k; ++r)
+            for (int q = 0; q < g.n_data; ++q)
+                if (lz[(size_t)r * g.n_data + q] & 1) packed[(size_t)r * W + q / 64] |= 1ull << (q % 64);
+        G->lz_arena.release();
+        g.lz = G->lz_arena.upload(packed);
+        g.k = k;
+    });
+}
+
+int qd_graph_set_priors(qd_graph* G, const double* probs) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        if (!probs) throw Fail(-50, "null channel_probs");
+        DevGraph& g = G->dg;
+        std::vector<double> ms64(g.n_pad, 0.0), ps64(g.n_pad, 0.0);
+        std::vector<float> ms32(g.n_pad, 0.0f), ps32(g.n_pad, 0.0f);
+        for (int j = 0; j < g.n; ++j) {
+            const double p = probs[j];
+            if (!(p >= 0.0 && p <= 1.0)) throw Fail(-51, "channel probability outside [0, 1]");
+            ms64[j] = std::log((1 - p) / p);   // ldpc v1: log((1-p)/p)
+            ps64[j] = p / (1 - p);             // ldpc v1: p/(1-p)
+            ms32[j] = (float)ms64[j];
+            ps32[j] = (float)ps64[j];
+        }
+        G->prior_arena.release();
+        g.prior[QD_MIN_SUM][QD_F64] = G->prior_arena.upload(ms64);
+        g.prior[QD_MIN_SUM][QD_F32] = G->prior_arena.upload(ms32);
+        g.prior[QD_PRODUCT_SUM][QD_F64] = G->prior_arena.upload(ps64);
+        g.prior[QD_PRODUCT_SUM][QD_F32] = G->prior_arena.upload(ps32);
+        G->has_priors = true;
+    });
+}
+
+int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* syn, const uint8_t* base,
+                           const uint8_t* readout, uint8_t* x_out, uint8_t* corr_out, void* llr_out, int32_t* iters,
+                           uint8_t* status, int32_t* ssf_steps, uint8_t* fail, void* stream) {
+    return guarded([&] {
+        check_graph(G);
+        check_params(G, p);
+        if (B < 0) throw Fail(-8, "negative batch");
+        set_device(G);
+        DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
+        const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream);
+        if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
+int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* syn, const uint8_t* base,
+                    const uint8_t* readout, uint8_t* x_out, uint8_t* corr_out, void* llr_out, int32_t* iters,
+                    uint8_t* status, int32_t* ssf_steps, uint8_t* fail) {
+    return guarded([&] {
+        check_graph(G);
+        check_params(G, p);
+        if (B < 0) throw Fail(-8, "negative batch");
+        if (B == 0) return;
+        set_device(G);
+        const DevGraph& g = G->dg;
+        const size_t tsz = p->precision == QD_F32 ? 4 : 8;
+        // workspace layout (each region 256-B aligned)
+        struct Reg { size_t off, bytes; };
+        size_t off = 0;
+        auto reg = [&](size_t bytes, bool on) {
+            Reg r{off, on ? bytes : 0};
+            if (on) off += (bytes + 255) / 256 * 256;
+            return r;
+        };
+        const Reg r_syn = reg((size_t)B * g.m, syn != nullptr);
+        const Reg r_base = reg((size_t)B * g.n_data, base != nullptr);
+        const Reg r_rd = reg((size_t)B * g.n_data, readout != nullptr);
+        const Reg r_x = reg((size_t)B * g.n, x_out != nullptr);
+        const Reg r_corr = reg((size_t)B * g.n_data, corr_out != nullptr);
+        const Reg r_llr = reg((size_t)B * g.n * tsz, llr_out != nullptr);
+        const Reg r_it = reg((size_t)B * 4, iters != nullptr);
+        const Reg r_st = reg((size_t)B, status != nullptr);
+        const Reg r_ss = reg((size_t)B * 4, ssf_steps != nullptr);
+        const Reg r_fl = reg((size_t)B, fail != nullptr);
+        if (off > G->ws_bytes) {
+            if (G->ws) hip_check(hipFree(G->ws), "hipFree");
+            G->ws = nullptr;
+            G->ws_bytes = 0;
+            hip_check(hipMalloc(&G->ws, off), "hipMalloc workspace");
+            G->ws_bytes = off;
+        }
+        auto* w = static_cast<uint8_t*>(G->ws);
+        auto dptr = [&](const Reg& r) -> void* { return r.bytes ? (void*)(w + r.off) : nullptr; };
+        hipStream_t s = G->stream;
+        if (syn) hip_check(hipMemcpyAsync(dptr(r_syn), syn, r_syn.bytes, hipMemcpyHostToDevice, s), "H2D syn");
+        if (base) hip_check(hipMemcpyAsync(dptr(r_base), base, r_base.bytes, hipMemcpyHostToDevice, s), "H2D base");
+        if (readout) hip_check(hipMemcpyAsync(dptr(r_rd), readout, r_rd.bytes, hipMemcpyHostToDevice, s), "H2D readout");
+        DecodeArgs a = make_args(G, p, B, (const uint8_t*)dptr(r_syn), (const uint8_t*)dptr(r_base),
+                                 (const uint8_t*)dptr(r_rd), (uint8_t*)dptr(r_x), (uint8_t*)dptr(r_corr), dptr(r_llr),
+                                 (int32_t*)dptr(r_it), (uint8_t*)dptr(r_st), (int32_t*)dptr(r_ss), (uint8_t*)dptr(r_fl));
+        const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s);
+        if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
+        auto d2h = [&](void* h, const Reg& r, const char* what) {
+            if (h) hip_check(hipMemcpyAsync(h, dptr(r), r.bytes, hipMemcpyDeviceToHost, s), what);
+        };
+        d2h(x_out, r_x, "D2H x");
+        d2h(corr_out, r_corr, "D2H corr");
+        d2h(llr_out, r_llr, "D2H llr");
+        d2h(iters, r_it, "D2H iters");
+        d2h(status, r_st, "D2H status");
+        d2h(ssf_steps, r_ss, "D2H ssf_steps");
+        d2h(fail, r_fl, "D2H fail");
+        hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    });
+}
+
+int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double p_meas, uint32_t seed,
+                             uint32_t stream_id, int64_t shot0, int64_t B, uint8_t* syn, uint8_t* readout,
+                             void* stream) {
+    return guarded([&] {
+        check_graph(G);
+        if (rounds < 0 || B < 0 || !syn || !readout) throw Fail(-60, "invalid sampler arguments");
+        if (G->dg.fold_blocks != 1 || G->dg.n_data != G->dg.n) throw Fail(-61, "sampler needs a plain code graph (H = Hz)");
+        auto thr = [](double p) -> uint32_t {
+            if (!(p > 0)) return 0u;
+            const double v = std::floor(p * 4294967296.0);
+            return v >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)v;
+        };
+        set_device(G);
+        const int rc = launch_sample_storage(G->dg, rounds, thr(2.0 * p_data / 3.0), thr(p_meas), seed, stream_id,
+                                             shot0, B, syn, readout, G->num_cus, (hipStream_t)stream);
+        if (rc != 0) throw Fail(-102, std::string("sampler launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
+int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream) {
+    return guarded([&] {
+        if (B < 0 || (B > 0 && (!flags || !out))) throw Fail(-70, "invalid count arguments");
+        const int rc = launch_count_flags(flags, B, mask, out, (hipStream_t)stream);
+        if (rc != 0) throw Fail(-103, std::string("count launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// qdec_internal.h -- device-side graph description shared by the host ABI
+// (qdec_abi.cpp) and the kernels (qdec_bp.hip, qdec_sample.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qdec {
+
+constexpr int kWave = 64;        // CDNA wavefront
+constexpr int kDR = 8;           // max check degree of the wave kernels
+constexpr int kDC = 4;           // max variable degree of the wave kernels
+constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
+constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
+constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
+
+// LDS stride, in elements, of a per-lane block of D values of type T, chosen so a
+// wave reading its 64 blocks with 16-byte ds_read_b128 is bank-conflict free:
+// dword stride a multiple of 4 with an odd quotient (16 lanes cover 64 banks).
+template <typename T, int D>
+constexpr int lds_stride() {
+    int dw = (int)((D * sizeof(T) + 3) / 4);
+    dw = (dw + 3) / 4 * 4;
+    if ((dw / 4) % 2 == 0) dw += 4;
+    return dw * 4 / (int)sizeof(T);
+}
+
+// Slot tables depend on the element stride, i.e. on the precision.
+struct SlotTables {
+    const uint16_t* r_cslot;  // [kDR][m_pad]  c2v element written by check i, edge k
+    const uint16_t* c_rslot;  // [kDC][n_pad]  v2c element written by variable j, edge k
+};
+
+struct DevGraph {
+    int m, n, m_pad, n_pad;       // pads: multiples of 64
+    int n_data, fold_blocks;
+    int max_rdeg, max_cdeg;
+    const uint8_t* r_deg;         // [m_pad]
+    const uint16_t* r_col;        // [kDR][m_pad]  column of edge k of check i (pad -> n_pad)
+    const uint8_t* c_deg;         // [n_pad]
+    SlotTables slots[2];          // [QD_F64], [QD_F32]
+    const void* prior[2][2];      // [method][precision] initial message per column, [n_pad]
+    // CSR copy (sampler; generic paths)
+    const int32_t* row_ptr;
+    const int32_t* col_idx;
+    // flip sets (SSF)
+    int n_gen, g_pad, g_wmax;
+    const uint8_t* g_w;           // [g_pad]
+    const uint16_t* g_q;          // [kGenW][g_pad]   qubit (column) k of generator g
+    const uint8_t* g_nlc;         // [g_pad]
+    const uint16_t* g_lc;         // [kGenLC][g_pad]  local check c of generator g
+    const uint32_t* g_qmask;      // [kGenW][g_pad]   local-check mask of qubit k
+    // logicals (fused failure check)
+    int k, lz_words;
+    const uint64_t* lz;           // [k][lz_words]    bit q%64 of word q/64
+};
+
+struct DecodeArgs {
+    int64_t B;
+    int max_iter, ssf, ssf_max_steps, syn_flags;
+    double ms_scaling;
+    const uint8_t* syn;
+    const uint8_t* base;
+    const uint8_t* readout;
+    uint8_t* x_out;
+    uint8_t* corr_out;
+    void* llr_out;
+    int32_t* iters;
+    uint8_t* status;
+    int32_t* ssf_steps;
+    uint8_t* fail;
+};
+
+// Launchers (qdec_bp.hip / qdec_sample.hip).  Return hipError_t as int.
+int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a,
+                  int num_cus, hipStream_t stream);
+int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,
+                          uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
+                          uint8_t* syn, uint8_t* readout, int num_cus, hipStream_t stream);
+int launch_count_flags(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, hipStream_t stream);
+
+}  // namespace qdec

@@ -1,0 +1,220 @@
+"""Batched GPU decoder over one parity-check graph (host side of the C ABI).
+
+``Decoder`` owns a ``qd_graph`` on one device: the matrix, its priors, optional
+flip sets (SSF) and logicals (fused failure check).  ``decode`` works on host
+numpy arrays (the ldpc-like path, H2D/D2H inside the library); ``decode_device``
+works on device-resident torch tensors and only enqueues work on the current
+torch stream (the throughput path).
+
+Decode contract (one call = B shots; identical to oracle/qdec_oracle.c):
+  1. s = syn (or 0); with syn_flags: s ^= H[:, :n_data] (base ^ readout)
+  2. BP (ldpc v1 loops; min-sum log domain or product-sum) until H x = s or max_iter
+  3. if ssf and not converged: small-set-flip on the residual s ^ H x
+  4. corr = base ^ fold(x),   fold(x)[q] = xor_t x[t*n_data + q]
+  5. fail = any_r (Lz[r] . (readout ^ corr)) mod 2
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _abi
+
+__all__ = ["Decoder", "parse_bp_method", "as_csr01"]
+
+_PS_NAMES = {"ps", "product_sum", "prod_sum", "0", "prod sum", "product sum"}
+_MS_NAMES = {"ms", "minimum_sum", "min_sum", "1", "minimum sum", "min sum",
+             "msl", "minimum_sum_log", "ms_log", "min_sum_log", "3", "minimum sum_log", "minimum sum log"}
+_PSL_NAMES = {"ps_log", "product_sum_log", "prod_sum_log", "2", "psl"}
+
+
+def parse_bp_method(method) -> int:
+    """ldpc v1 bp_method names -> QD_*.  'ms' and 'msl' both mean min-sum in the
+    log domain (ldpc v1 maps min_sum to its log variant)."""
+    key = str(method).strip().lower()
+    if key in _PS_NAMES:
+        return _abi.QD_PRODUCT_SUM
+    if key in _MS_NAMES:
+        return _abi.QD_MIN_SUM
+    if key in _PSL_NAMES:
+        raise NotImplementedError("bp_method 'ps_log' (product-sum, log domain) is not implemented by this build; "
+                                  "use 'ps' or 'ms'")
+    raise ValueError(f"unknown bp_method {method!r}")
+
+
+def parse_precision(precision) -> int:
+    key = str(precision).lower()
+    if key in ("f32", "fp32", "float32", "float"):
+        return _abi.QD_F32
+    if key in ("f64", "fp64", "float64", "double"):
+        return _abi.QD_F64
+    raise ValueError(f"unknown precision {precision!r}")
+
+
+def as_csr01(H) -> sp.csr_matrix:
+    """Any dense/sparse 0/1 matrix -> canonical CSR (sorted, deduplicated mod 2)."""
+    if sp.issparse(H):
+        M = sp.csr_matrix(H, dtype=np.int64)
+    else:
+        M = sp.csr_matrix(np.asarray(H, dtype=np.int64))
+    M.sum_duplicates()
+    M.data %= 2
+    M.eliminate_zeros()
+    M.sort_indices()
+    M.data[:] = 1
+    return M
+
+
+class Decoder:
+    def __init__(self, H, channel_probs, *, method="ms", precision="f32", max_iter: int = 0,
+                 ms_scaling: float = 0.0, flip_sets=None, ssf: bool | None = None, ssf_max_steps: int = 0,
+                 logicals=None, n_data: int | None = None, fold_blocks: int = 1, device: int = 0):
+        self._lib = _abi.load()
+        H = as_csr01(H)
+        self.H = H
+        self.m, self.n = H.shape
+        self.n_data = self.n if n_data is None else int(n_data)
+        self.fold_blocks = int(fold_blocks)
+        self.device = int(device)
+        self._handle = C.c_void_p()
+        rp = np.ascontiguousarray(H.indptr, dtype=np.int32)
+        ci = np.ascontiguousarray(H.indices, dtype=np.int32)
+        _abi.check(self._lib.qd_graph_create(self.m, self.n, _abi.ptr(rp), _abi.ptr(ci), self.n_data,
+                                             self.fold_blocks, self.device, C.byref(self._handle)),
+                   "qd_graph_create")
+        self.method = parse_bp_method(method)
+        self.precision = parse_precision(precision)
+        self.max_iter = int(max_iter)
+        self.ms_scaling = float(ms_scaling)
+        self.ssf_max_steps = int(ssf_max_steps)
+        self.has_flip_sets = False
+        if flip_sets is not None:
+            self.set_flip_sets(flip_sets)
+        self.ssf = bool(self.has_flip_sets if ssf is None else ssf)
+        self.k = 0
+        if logicals is not None:
+            self.set_logicals(logicals)
+        self.set_priors(channel_probs)
+
+    # ------------------------------------------------------------ graph data
+    def set_priors(self, channel_probs) -> None:
+        p = np.ascontiguousarray(np.broadcast_to(np.asarray(channel_probs, dtype=np.float64), (self.n,)))
+        self.channel_probs = p.copy()
+        _abi.check(self._lib.qd_graph_set_priors(self._handle, _abi.ptr(p)), "qd_graph_set_priors")
+
+    def set_flip_sets(self, generators) -> None:
+        G = as_csr01(generators)
+        if G.shape[1] != self.n:
+            raise ValueError("flip-set generators must have one column per decoding column")
+        gp = np.ascontiguousarray(G.indptr, dtype=np.int32)
+        gi = np.ascontiguousarray(G.indices, dtype=np.int32)
+        _abi.check(self._lib.qd_graph_set_flipsets(self._handle, G.shape[0], _abi.ptr(gp), _abi.ptr(gi)),
+                   "qd_graph_set_flipsets")
+        self.has_flip_sets = True
+
+    def set_logicals(self, lz) -> None:
+        lz = np.ascontiguousarray(np.asarray(lz.todense() if sp.issparse(lz) else lz) % 2, dtype=np.uint8)
+        if lz.ndim != 2 or lz.shape[1] != self.n_data:
+            raise ValueError("logicals must be k x n_data")
+        _abi.check(self._lib.qd_graph_set_logicals(self._handle, lz.shape[0], _abi.ptr(lz)), "qd_graph_set_logicals")
+        self.k = lz.shape[0]
+
+    def _params(self, syn_flags: int = 0, ssf: bool | None = None) -> _abi.QdParams:
+        return _abi.QdParams(self.max_iter, self.method, self.precision,
+                             int(self.ssf if ssf is None else ssf), self.ssf_max_steps, int(syn_flags),
+                             self.ms_scaling)
+
+    @property
+    def llr_dtype(self):
+        return np.float32 if self.precision == _abi.QD_F32 else np.float64
+
+    # ------------------------------------------------------------ decoding
+    def decode(self, syn=None, *, base=None, readout=None, syn_flags: int = 0, ssf: bool | None = None,
+               want=("x", "corr", "iters", "status", "ssf_steps", "fail")) -> dict:
+        """Decode B shots from host arrays; returns numpy arrays for `want`
+        (any of x, corr, llr, iters, status, ssf_steps, fail)."""
+        def u8(a, cols):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(np.asarray(a), dtype=np.uint8)
+            return a.reshape(-1, cols)
+        syn = u8(syn, self.m)
+        base = u8(base, self.n_data)
+        readout = u8(readout, self.n_data)
+        B = next(a.shape[0] for a in (syn, base, readout) if a is not None)
+        for a in (syn, base, readout):
+            if a is not None and a.shape[0] != B:
+                raise ValueError("inconsistent batch sizes")
+        out = {}
+        if "x" in want:
+            out["x"] = np.empty((B, self.n), np.uint8)
+        if "corr" in want:
+            out["corr"] = np.empty((B, self.n_data), np.uint8)
+        if "llr" in want:
+            out["llr"] = np.empty((B, self.n), self.llr_dtype)
+        if "iters" in want:
+            out["iters"] = np.empty(B, np.int32)
+        if "status" in want:
+            out["status"] = np.empty(B, np.uint8)
+        if "ssf_steps" in want:
+            out["ssf_steps"] = np.empty(B, np.int32)
+        if "fail" in want:
+            out["fail"] = np.empty(B, np.uint8)
+        prm = self._params(syn_flags, ssf)
+        g = out.get
+        _abi.check(self._lib.qd_decode_batch(
+            self._handle, C.byref(prm), B, _abi.ptr(syn), _abi.ptr(base), _abi.ptr(readout),
+            _abi.ptr(g("x")), _abi.ptr(g("corr")), _abi.ptr(g("llr")), _abi.ptr(g("iters")),
+            _abi.ptr(g("status")), _abi.ptr(g("ssf_steps")), _abi.ptr(g("fail"))), "qd_decode_batch")
+        return out
+
+    def decode_device(self, B: int, *, syn=None, base=None, readout=None, x=None, corr=None, llr=None,
+                      iters=None, status=None, ssf_steps=None, fail=None, syn_flags: int = 0,
+                      ssf: bool | None = None, stream=None) -> None:
+        """Enqueue a decode of B device-resident shots (torch tensors or raw
+        device pointers) on `stream` (default: torch's current stream)."""
+        if stream is None:
+            stream = _current_stream(self.device)
+        prm = self._params(syn_flags, ssf)
+        _abi.check(self._lib.qd_decode_batch_device(
+            self._handle, C.byref(prm), int(B), _abi.ptr(syn), _abi.ptr(base), _abi.ptr(readout), _abi.ptr(x),
+            _abi.ptr(corr), _abi.ptr(llr), _abi.ptr(iters), _abi.ptr(status), _abi.ptr(ssf_steps), _abi.ptr(fail),
+            C.c_void_p(stream)), "qd_decode_batch_device")
+
+    def sample_storage_device(self, rounds: int, p_data: float, p_meas: float, seed: int, stream_id: int,
+                              shot0: int, B: int, syn, readout, stream=None) -> None:
+        """Storage-experiment sampler (H must be the plain Hz graph)."""
+        if stream is None:
+            stream = _current_stream(self.device)
+        _abi.check(self._lib.qd_sample_storage_device(
+            self._handle, int(rounds), float(p_data), float(p_meas), int(seed) & 0xFFFFFFFF,
+            int(stream_id) & 0xFFFFFFFF, int(shot0), int(B), _abi.ptr(syn), _abi.ptr(readout), C.c_void_p(stream)),
+            "qd_sample_storage_device")
+
+    def close(self) -> None:
+        if getattr(self, "_handle", None) and self._handle.value:
+            self._lib.qd_graph_destroy(self._handle)
+            self._handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def count_flags_device(flags, B: int, mask: int, out, stream=None, device: int = 0) -> None:
+    """out (device int64[1]) += #{b : flags[b] & mask}."""
+    lib = _abi.load()
+    if stream is None:
+        stream = _current_stream(device)
+    _abi.check(lib.qd_count_flags_device(_abi.ptr(flags), int(B), int(mask) & 0xFF, _abi.ptr(out),
+                                         C.c_void_p(stream)), "qd_count_flags_device")
+
+
+def _current_stream(device: int) -> int:
+    if _abi.torch is not None and _abi.torch.cuda.is_available():
+        return int(_abi.torch.cuda.current_stream(device).cuda_stream)
+    return 0

@@ -1,0 +1,131 @@
+/*
+ * qdec.h -- C ABI of libqdec_hip.so, the MI355X (gfx950) BP + small-set-flip
+ * syndrome decoder.
+ *
+ * This is the drop-in boundary for the reference's decoding hot path.  In the
+ * reference (qldpc/exp_ldpc @ 2025-02-21) that boundary is the third-party
+ * `ldpc` v1 decoder-object API, called only from python/qldpc/misc/_experiment.py:
+ *   - construction  bposd_decoder(H, error_rate=.., **opts)     _experiment.py:23-27, 96-100
+ *                   bposd_decoder(H, channel_probs=.., **opts)  _experiment.py:37-40
+ *                   bposd_decoder(H, channel_prior=.., **opts)  _experiment.py:77
+ *                   bp_decoder(H, channel_probs=.., **opts)     _experiment.py:110-113, 137-140
+ *   - decode        .decode(syndrome) -> ndarray[n]             _experiment.py:51, 59, 82, 117, 125, 149
+ *   - per-shot logical check  any(GF2(Lz) @ GF2(readout))       _experiment.py:209
+ * Each entry point below names the reference interface it replaces.  The Python
+ * binding (exp_ldpc_amd/_abi.py, ctypes) and the ldpc-v1-compatible classes are
+ * described in INTEGRATION.md.
+ *
+ * Conventions: plain pointers and sizes; no C++ exceptions cross the ABI; status
+ * 0 = OK, negative = error (message via qd_last_error(), thread-local).  The
+ * library owns device copies of the graph; the caller owns every buffer it
+ * passes.  A handle is used from one host thread at a time; one handle per
+ * device for multi-GPU.
+ */
+#ifndef QDEC_H
+#define QDEC_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QDEC_ABI_VERSION 1
+
+typedef struct qd_graph qd_graph;
+
+enum qd_method { QD_PRODUCT_SUM = 0, QD_MIN_SUM = 1 };      /* ldpc bp_method 'ps' / 'ms','msl' */
+enum qd_precision { QD_F64 = 0, QD_F32 = 1 };               /* message arithmetic */
+enum qd_syn_flags { QD_SYN_ADD_BASE = 1, QD_SYN_ADD_READOUT = 2 };
+enum qd_status_bits { QD_ST_BP_CONVERGED = 1, QD_ST_SATISFIED = 2 };
+
+typedef struct qd_params {
+    int32_t max_iter;      /* <= 0 -> n (ldpc v1: max_iter=0 means n) */
+    int32_t method;        /* enum qd_method */
+    int32_t precision;     /* enum qd_precision */
+    int32_t ssf;           /* 1: small-set-flip on shots BP did not converge (needs flip sets) */
+    int32_t ssf_max_steps; /* <= 0: unbounded (terminates: |residual| strictly decreases) */
+    int32_t syn_flags;     /* enum qd_syn_flags: syndrome ^= H[:, :n_data] (base ^ readout) */
+    double ms_scaling;     /* 0 -> alpha_t = 1 - 2^-t (ldpc ms_scaling_factor=0) */
+} qd_params;
+
+/* Version / device discovery. */
+int qd_abi_version(void);
+int qd_device_count(void);
+const char* qd_last_error(void);
+
+/* Replaces the ldpc constructor's copy of H into mod2sparse (_experiment.py:23,
+ * 37, 77, 96, 110, 137).  H is m x n CSR with column indices sorted within each
+ * row (row_ptr[m+1], col_idx[row_ptr[m]]).  Columns t*n_data + q (t <
+ * fold_blocks) fold onto data qubit q (SpacetimeCode.final_correction,
+ * spacetime_code.py:81-84); fold_blocks = 1, n_data = n for a plain code.  The
+ * graph is uploaded to `device` (HIP ordinal). */
+int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx,
+                    int32_t n_data, int32_t fold_blocks, int32_t device, qd_graph** out);
+int qd_graph_destroy(qd_graph* g);
+
+/* Flip sets for small-set-flip: generator rows (CSR over H's columns; for the
+ * storage experiment the X-check rows of Hx).  Each generator must have <= 8
+ * qubits whose checks in H number <= 32.  No reference counterpart (SSF is
+ * absent from the reference). */
+int qd_graph_set_flipsets(qd_graph* g, int32_t n_gen, const int32_t* gen_ptr, const int32_t* gen_idx);
+
+/* Logical operators for the fused failure check, dense 0/1 k x n_data (the `LZ`
+ * rows of the qecc file; replaces GF2(logicals.z) @ GF2(readout) at
+ * _experiment.py:209). */
+int qd_graph_set_logicals(qd_graph* g, int32_t k, const uint8_t* lz);
+
+/* Per-column error probabilities (ldpc `error_rate` broadcast / `channel_probs`;
+ * reference call sites _experiment.py:23-27, 37-40, 74-77, 106-113).  Converted
+ * on the host to the ldpc initial messages log((1-p)/p) (min-sum) and p/(1-p)
+ * (product-sum) in both precisions. */
+int qd_graph_set_priors(qd_graph* g, const double* channel_probs);
+
+/* Batched replacement of B calls to .decode(syndrome) (_experiment.py:82, 117,
+ * 125, ...), plus the fused fold and logical check.  Host buffers; synchronous.
+ *   syn       uint8 [B][m]       syndrome bits (nullable when syn_flags set)
+ *   base      uint8 [B][n_data]  xor-ed into corr_out (and into the syndrome with
+ *                                QD_SYN_ADD_BASE); nullable
+ *   readout   uint8 [B][n_data]  data readout for the failure flag (and the
+ *                                syndrome with QD_SYN_ADD_READOUT); nullable
+ * outputs (each nullable):
+ *   x_out     uint8 [B][n]       decoding (BP hard decision, SSF applied) = ldpc .decode() result
+ *   corr_out  uint8 [B][n_data]  base ^ fold(x_out)
+ *   llr_out   [B][n] float (QD_F32) or double (QD_F64): ldpc .log_prob_ratios
+ *   iters     int32 [B]          ldpc .iter
+ *   status    uint8 [B]          QD_ST_BP_CONVERGED (= ldpc .converge) | QD_ST_SATISFIED
+ *   ssf_steps int32 [B]          flips applied by SSF
+ *   fail      uint8 [B]          any(Lz (readout ^ corr_out)) mod 2 (needs logicals+readout) */
+int qd_decode_batch(qd_graph* g, const qd_params* prm, int64_t B,
+                    const uint8_t* syn, const uint8_t* base, const uint8_t* readout,
+                    uint8_t* x_out, uint8_t* corr_out, void* llr_out,
+                    int32_t* iters, uint8_t* status, int32_t* ssf_steps, uint8_t* fail);
+
+/* Same contract on device-resident buffers (HBM), enqueued on `stream`
+ * (hipStream_t; NULL = default stream); returns after the launch. */
+int qd_decode_batch_device(qd_graph* g, const qd_params* prm, int64_t B,
+                           const uint8_t* syn, const uint8_t* base, const uint8_t* readout,
+                           uint8_t* x_out, uint8_t* corr_out, void* llr_out,
+                           int32_t* iters, uint8_t* status, int32_t* ssf_steps, uint8_t* fail,
+                           void* stream);
+
+/* Replaces Stim's compile_sampler().sample(B) + StorageSim slicing +
+ * _spacetime_syndrome (_experiment.py:196-207, storage_sim.py:187-196,
+ * spacetime_code.py:98-119) for the storage experiment under
+ * depolarizing_noise(p_data, pm=p_meas) (noise_model.py:117-123).  The graph must
+ * be a plain code (fold_blocks = 1): H = Hz.  Writes, on device:
+ *   syn     uint8 [B][(rounds+1)*m]  spacetime (difference) syndrome
+ *   readout uint8 [B][n]             transversal Z readout
+ * Philox4x32-10 keyed (seed, stream_id), counter (word, event, shot): results
+ * do not depend on how shots are split across calls or devices. */
+int qd_sample_storage_device(qd_graph* g, int32_t rounds, double p_data, double p_meas,
+                             uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
+                             uint8_t* syn, uint8_t* readout, void* stream);
+
+/* Device-side sum of a uint8 flag array (failure / status counts) into *out
+ * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */
+int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,194 @@
+"""GPU parity: the HIP decoder (through the C ABI) against the CPU oracle on the
+same seeded inputs.  Bar: bit-exact hard decisions, iteration counts, status,
+SSF steps, corrections and failure flags; min-sum LLRs bit-exact; product-sum
+LLRs (ldpc's log(1/ratio) output, computed with the device log) within
+rtol 1e-12 (f64) / 1e-6 (f32)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import load_checks
+
+pytestmark = pytest.mark.gpu
+
+HX, HZ = load_checks("hgp_12_3_4_s1234")
+
+
+def _errors(rng, B, n, p):
+    return (rng.random((B, n)) < p).astype(np.uint8)
+
+
+def _spacetime(R):
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    return SpacetimeCode(HZ, R).spacetime_check_matrix
+
+
+def _cmp_llr(a, b, method, precision):
+    if method == "ms":
+        assert np.array_equal(a.astype(np.float64), b), "min-sum LLRs must be bit-exact"
+    else:
+        rtol = 1e-12 if precision == "f64" else 1e-6
+        a = a.astype(np.float64)
+        fin = np.isfinite(b)
+        assert np.array_equal(np.isfinite(a), fin)
+        assert np.array_equal(a[~fin], b[~fin])
+        np.testing.assert_allclose(a[fin], b[fin], rtol=rtol, atol=0)
+
+
+@pytest.mark.parametrize("method", ["ms", "ps"])
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("shape", ["R0", "R1"])
+def test_bp_parity(gpu_available, oracle_lib, method, precision, shape):
+    from exp_ldpc_amd.decoder import Decoder
+    H = HZ if shape == "R0" else _spacetime(1)
+    m, n = H.shape
+    rng = np.random.default_rng(hash((method, precision, shape)) % 2**32)
+    B = 3000
+    p = np.where(rng.random(B) < 0.5, 0.01, 0.04)[:, None]
+    e = (rng.random((B, n)) < p).astype(np.uint8)
+    syn = ((sp.csr_matrix(H) @ e.T).T % 2).astype(np.uint8)
+    prior = 0.02
+    dec = Decoder(H, prior, method=method, precision=precision, max_iter=40)
+    got = dec.decode(syn, want=("x", "llr", "iters", "status"))
+    ref = oracle_lib.decode(H, prior, syn, method=method, precision=precision, max_iter=40)
+    assert np.array_equal(got["iters"], ref["iters"])
+    assert np.array_equal(got["status"], ref["status"])
+    assert np.array_equal(got["x"], ref["x"])
+    _cmp_llr(got["llr"], ref["llr"], method, precision)
+    # both converged and non-converged shots are exercised
+    conv = ref["status"] & 1
+    assert 0 < conv.mean() < 1
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("max_iter", [1, 3, 50])
+def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, code225):
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(max_iter)
+    B = 2000
+    rd = _errors(rng, B, 225, 0.03)
+    syn = ((HZ @ rd.T).T % 2).astype(np.uint8)
+    lz = code225.logicals.z
+    dec = Decoder(HZ, 0.02, method="ms", precision=precision, max_iter=max_iter, flip_sets=HX, logicals=lz)
+    got = dec.decode(syn, readout=rd, want=("x", "corr", "iters", "status", "ssf_steps", "fail"))
+    ref = oracle_lib.decode(HZ, 0.02, syn, method="ms", precision=precision, max_iter=max_iter, ssf=True, gens=HX,
+                            lz=lz, readout=rd, want_llr=False)
+    for key in ("x", "corr", "iters", "status", "ssf_steps", "fail"):
+        assert np.array_equal(got[key], ref[key]), key
+    assert ref["ssf_steps"].sum() > 0
+
+
+def test_ssf_bounded_steps(gpu_available, oracle_lib):
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(5)
+    rd = _errors(rng, 500, 225, 0.06)
+    syn = ((HZ @ rd.T).T % 2).astype(np.uint8)
+    for steps in (1, 2):
+        dec = Decoder(HZ, 0.03, method="ms", precision="f32", max_iter=2, flip_sets=HX, ssf_max_steps=steps)
+        got = dec.decode(syn, want=("x", "ssf_steps", "status"))
+        ref = oracle_lib.decode(HZ, 0.03, syn, method="ms", precision="f32", max_iter=2, ssf=True, gens=HX,
+                                ssf_max_steps=steps, want_llr=False)
+        assert got["ssf_steps"].max() <= steps
+        for key in ("x", "ssf_steps", "status"):
+            assert np.array_equal(got[key], ref[key]), key
+
+
+def test_spacetime_fold_and_fail(gpu_available, oracle_lib, code225):
+    """R=1 spacetime decode with the fused fold (SpacetimeCode.final_correction)
+    and failure flag."""
+    from exp_ldpc_amd.decoder import Decoder
+    H = _spacetime(1)
+    syn, rd = oracle_lib.sample_storage(HZ, 1, 0.02, 0.02, seed=3, stream=0, shot0=0, B=3000)
+    lz = code225.logicals.z
+    dec = Decoder(H, 2 * 0.02 / 3, method="ms", precision="f32", max_iter=30, n_data=225, fold_blocks=2, logicals=lz)
+    got = dec.decode(syn, readout=rd, want=("x", "corr", "iters", "status", "fail"))
+    ref = oracle_lib.decode(H, 2 * 0.02 / 3, syn, method="ms", precision="f32", max_iter=30, n_data=225,
+                            fold_blocks=2, lz=lz, readout=rd, want_llr=False)
+    for key in ("x", "corr", "iters", "status", "fail"):
+        assert np.array_equal(got[key], ref[key]), key
+    fold = (ref["x"][:, :225] ^ ref["x"][:, 225:450])
+    assert np.array_equal(got["corr"], fold)
+
+
+def test_hybrid_stage2_syndrome_from_vectors(gpu_available, oracle_lib, code225):
+    """bpssf_hybrid stage 2: syndrome = Hz (readout ^ stage-1 correction)."""
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(11)
+    B = 1500
+    rd = _errors(rng, B, 225, 0.03)
+    c1 = _errors(rng, B, 225, 0.01)
+    lz = code225.logicals.z
+    dec = Decoder(HZ, 0.02, method="ms", precision="f32", max_iter=20, flip_sets=HX, logicals=lz)
+    got = dec.decode(None, base=c1, readout=rd, syn_flags=3, want=("x", "corr", "iters", "status", "ssf_steps", "fail"))
+    ref = oracle_lib.decode(HZ, 0.02, None, method="ms", precision="f32", max_iter=20, ssf=True, gens=HX, lz=lz,
+                            base=c1, readout=rd, syn_flags=3, B=B, want_llr=False)
+    for key in ("x", "corr", "iters", "status", "ssf_steps", "fail"):
+        assert np.array_equal(got[key], ref[key]), key
+
+
+@pytest.mark.parametrize("rounds", [0, 1, 2, 3])
+def test_sampler_parity(gpu_available, oracle_lib, rounds):
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    dec = Decoder(HZ, 0.01)
+    B, shot0 = 4000, 12345
+    m, n = HZ.shape
+    syn = torch.empty((B, (rounds + 1) * m), dtype=torch.uint8, device="cuda")
+    rd = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+    dec.sample_storage_device(rounds, 0.03, 0.02, seed=20250221, stream_id=4, shot0=shot0, B=B, syn=syn, readout=rd)
+    torch.cuda.synchronize()
+    rs, rr = oracle_lib.sample_storage(HZ, rounds, 0.03, 0.02, seed=20250221, stream=4, shot0=shot0, B=B)
+    assert np.array_equal(syn.cpu().numpy(), rs)
+    assert np.array_equal(rd.cpu().numpy(), rr)
+    # sharding invariance: the second half sampled alone equals the tail
+    syn2 = torch.empty((B // 2, (rounds + 1) * m), dtype=torch.uint8, device="cuda")
+    rd2 = torch.empty((B // 2, n), dtype=torch.uint8, device="cuda")
+    dec.sample_storage_device(rounds, 0.03, 0.02, seed=20250221, stream_id=4, shot0=shot0 + B // 2, B=B // 2,
+                              syn=syn2, readout=rd2)
+    torch.cuda.synchronize()
+    assert np.array_equal(syn2.cpu().numpy(), rs[B // 2:])
+
+
+def test_edge_cases(gpu_available, oracle_lib):
+    from exp_ldpc_amd.decoder import Decoder
+    dec = Decoder(HZ, 0.01, method="ms", precision="f32", max_iter=0, flip_sets=HX)
+    # all-zero syndrome: trivial decode converges at iteration 1 (no ldpc shortcut)
+    z = np.zeros((3, HZ.shape[0]), np.uint8)
+    out = dec.decode(z, want=("x", "iters", "status"))
+    assert not out["x"].any() and (out["iters"] == 1).all() and (out["status"] == 3).all()
+    # single shot, max_iter = 0 -> n
+    rng = np.random.default_rng(2)
+    s = rng.integers(0, 2, (1, HZ.shape[0])).astype(np.uint8)
+    got = dec.decode(s, want=("x", "iters", "status", "ssf_steps"))
+    ref = oracle_lib.decode(HZ, 0.01, s, method="ms", precision="f32", max_iter=0, ssf=True, gens=HX, want_llr=False)
+    for key in ("x", "iters", "status", "ssf_steps"):
+        assert np.array_equal(got[key], ref[key]), key
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_irregular_codes(gpu_available, oracle_lib, seed):
+    """Ragged degrees (1..8 per check, 0..4 per variable), odd sizes."""
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(seed)
+    m, n = int(rng.integers(20, 200)), int(rng.integers(30, 500))
+    rows = []
+    colcount = np.zeros(n, int)
+    for i in range(m):
+        d = int(rng.integers(1, 9))
+        cand = [j for j in rng.permutation(n) if colcount[j] < 4][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    from exp_ldpc_amd.codes import make_check_matrix
+    H = make_check_matrix(rows, n)
+    e = _errors(rng, 1000, n, 0.03)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.uniform(0.005, 0.1, n)
+    for method in ("ms", "ps"):
+        for precision in ("f32", "f64"):
+            dec = Decoder(H, probs, method=method, precision=precision, max_iter=25)
+            got = dec.decode(syn, want=("x", "llr", "iters", "status"))
+            ref = oracle_lib.decode(H, probs, syn, method=method, precision=precision, max_iter=25)
+            for key in ("x", "iters", "status"):
+                assert np.array_equal(got[key], ref[key]), (method, precision, key)
+            _cmp_llr(got["llr"], ref["llr"], method, precision)
