@@ -81,6 +81,9 @@ struct qd_graph {
     // workspace for the host-buffer API (grow only)
     void* ws = nullptr;
     size_t ws_bytes = 0;
+    // SSF work queue scratch (grow only): count | idx[B] | x[B][n] | r[B][m]
+    void* qws = nullptr;
+    int64_t q_cap = 0;
 };
 
 namespace {
@@ -96,8 +99,11 @@ void build_tables(qd_graph* G, int m, int n) {
     DevGraph& g = G->dg;
     g.m = m;
     g.n = n;
-    g.m_pad = std::max(64, (m + 63) / 64 * 64);
-    g.n_pad = std::max(64, (n + 63) / 64 * 64);
+    int rc = 0, rv = 0;
+    if (!pick_wave_shape(m, n, &rc, &rv))
+        throw Fail(-21, "graph too large for this build's wave kernel (m <= 256, n <= 576)");
+    g.m_pad = rc * 64;
+    g.n_pad = rv * 64;
     const auto& rp = G->row_ptr;
     const auto& ci = G->col_idx;
     const int E = rp[m];
@@ -120,19 +126,24 @@ void build_tables(qd_graph* G, int m, int n) {
     for (int j = 0; j < n; ++j) g.max_cdeg = std::max(g.max_cdeg, G->col_ptr[j + 1] - G->col_ptr[j]);
     if (g.max_rdeg > kDR || g.max_cdeg > kDC)
         throw Fail(-20, "graph degrees exceed this build's wave kernel (check degree <= 8, variable degree <= 4)");
-    if (g.m_pad / 64 > 4 || g.n_pad / 64 > 9)
-        throw Fail(-21, "graph too large for this build's wave kernel (m <= 256, n <= 576)");
 
     std::vector<uint8_t> r_deg(g.m_pad, 0), c_deg(g.n_pad, 0);
-    std::vector<uint16_t> r_col((size_t)kDR * g.m_pad, (uint16_t)g.n_pad);
+    // Pad edges (k >= degree, or padding rows/columns) point at per-lane dummies:
+    // column n_pad + lane (a zero byte of xh) and message slot <array end> + lane.
+    std::vector<uint16_t> r_col((size_t)kDR * g.m_pad);
+    for (size_t t = 0; t < r_col.size(); ++t) r_col[t] = (uint16_t)(g.n_pad + (t % g.m_pad) % 64);
     std::vector<uint16_t> r_cslot[2], c_rslot[2];
     const int DRS[2] = {drs<double>(), drs<float>()};
     const int DCS[2] = {dcs<double>(), dcs<float>()};
     for (int p = 0; p < 2; ++p) {
-        r_cslot[p].assign((size_t)kDR * g.m_pad, 0);
-        c_rslot[p].assign((size_t)kDC * g.n_pad, 0);
-        if ((size_t)g.m_pad * DRS[p] > 65535 || (size_t)g.n_pad * DCS[p] > 65535)
+        if ((size_t)g.m_pad * DRS[p] + 64 > 65535 || (size_t)g.n_pad * DCS[p] + 64 > 65535)
             throw Fail(-21, "graph too large for 16-bit LDS slots");
+        r_cslot[p].resize((size_t)kDR * g.m_pad);
+        for (size_t t = 0; t < r_cslot[p].size(); ++t)
+            r_cslot[p][t] = (uint16_t)(g.n_pad * DCS[p] + (t % g.m_pad) % 64);
+        c_rslot[p].resize((size_t)kDC * g.n_pad);
+        for (size_t t = 0; t < c_rslot[p].size(); ++t)
+            c_rslot[p][t] = (uint16_t)(g.m_pad * DRS[p] + (t % g.n_pad) % 64);
     }
     for (int i = 0; i < m; ++i) {
         r_deg[i] = (uint8_t)(rp[i + 1] - rp[i]);
@@ -164,6 +175,25 @@ void build_tables(qd_graph* G, int m, int n) {
     }
     g.row_ptr = G->arena.upload(G->row_ptr);
     g.col_idx = G->arena.upload(G->col_idx);
+}
+
+// Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.
+void attach_queue(qd_graph* G, DecodeArgs& a) {
+    if (!a.ssf || a.B <= 0) return;
+    const DevGraph& g = G->dg;
+    if (a.B > G->q_cap) {
+        if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
+        G->qws = nullptr;
+        G->q_cap = 0;
+        const size_t bytes = 256 + (size_t)a.B * (8 + (size_t)g.n + (size_t)g.m) + 256;
+        hip_check(hipMalloc(&G->qws, bytes), "hipMalloc queue");
+        G->q_cap = a.B;
+    }
+    auto* base = static_cast<uint8_t*>(G->qws);
+    a.q_count = reinterpret_cast<int32_t*>(base);
+    a.q_idx = reinterpret_cast<int64_t*>(base + 256);
+    a.q_x = base + 256 + (size_t)G->q_cap * 8;
+    a.q_r = a.q_x + (size_t)G->q_cap * g.n;
 }
 
 void check_graph(const qd_graph* g) {
@@ -273,6 +303,7 @@ int qd_graph_destroy(qd_graph* g) {
         g->lz_arena.release();
         g->prior_arena.release();
         if (g->ws) (void)hipFree(g->ws);
+        if (g->qws) (void)hipFree(g->qws);
         if (g->stream) (void)hipStreamDestroy(g->stream);
         delete g;
     });
@@ -284,11 +315,16 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         set_device(G);
         if (n_gen <= 0 || !gen_ptr || !gen_idx) throw Fail(-30, "invalid flip sets");
         DevGraph& g = G->dg;
-        const int gp = (n_gen + 63) / 64 * 64;
+        if (g.m_pad > 128 || n_gen > g.m_pad)
+            throw Fail(-36, "SSF supports graphs with m <= 128 and at most m_pad generators in this build");
+        const int gp = g.m_pad;
         std::vector<uint8_t> w(gp, 0), nlc(gp, 0);
         std::vector<uint16_t> q((size_t)kGenW * gp, 0), lc((size_t)kGenLC * gp, 0);
         std::vector<uint32_t> qm((size_t)kGenW * gp, 0);
-        int wmax = 0;
+        std::vector<uint32_t> lc8((size_t)(kGenLC / 4) * gp, 0);
+        for (int gi = 0; gi < gp; ++gi)
+            for (int c = 0; c < kGenLC; ++c) lc8[(size_t)(c / 4) * gp + gi] |= (uint32_t)g.m_pad << (8 * (c % 4));
+        int wmax = 0, nlcmax = 0;
         for (int gi = 0; gi < n_gen; ++gi) {
             const int a = gen_ptr[gi], b = gen_ptr[gi + 1];
             if (b < a) throw Fail(-31, "gen_ptr not monotone");
@@ -307,7 +343,12 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
             w[gi] = (uint8_t)wg;
             nlc[gi] = (uint8_t)checks.size();
             wmax = std::max(wmax, wg);
-            for (size_t c = 0; c < checks.size(); ++c) lc[c * gp + gi] = (uint16_t)checks[c];
+            nlcmax = std::max(nlcmax, (int)checks.size());
+            for (size_t c = 0; c < checks.size(); ++c) {
+                lc[c * gp + gi] = (uint16_t)checks[c];
+                uint32_t& word = lc8[(c / 4) * gp + gi];
+                word = (word & ~(0xffu << (8 * (c % 4)))) | ((uint32_t)checks[c] << (8 * (c % 4)));
+            }
             for (int k = 0; k < wg; ++k) {
                 const int qq = gen_idx[a + k];
                 q[(size_t)k * gp + gi] = (uint16_t)qq;
@@ -325,6 +366,8 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         g.g_q = G->flip_arena.upload(q);
         g.g_lc = G->flip_arena.upload(lc);
         g.g_qmask = G->flip_arena.upload(qm);
+        g.g_lc8 = G->flip_arena.upload(lc8);
+        g.g_nlcmax = nlcmax;
         g.n_gen = n_gen;
         g.g_pad = gp;
         g.g_wmax = wmax;
@@ -359,7 +402,9 @@ int qd_graph_set_priors(qd_graph* G, const double* probs) {
         std::vector<float> ms32(g.n_pad, 0.0f), ps32(g.n_pad, 0.0f);
         for (int j = 0; j < g.n; ++j) {
             const double p = probs[j];
-            if (!(p >= 0.0 && p <= 1.0)) throw Fail(-51, "channel probability outside [0, 1]");
+            // open interval: keeps every BP message finite (and NaN-free), the
+            // precondition of the kernels' min/med3 check-node formulation
+            if (!(p > 0.0 && p < 1.0)) throw Fail(-51, "channel probability outside (0, 1)");
             ms64[j] = std::log((1 - p) / p);   // ldpc v1: log((1-p)/p)
             ps64[j] = p / (1 - p);             // ldpc v1: p/(1-p)
             ms32[j] = (float)ms64[j];
@@ -383,6 +428,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         if (B < 0) throw Fail(-8, "negative batch");
         set_device(G);
         DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
+        attach_queue(G, a);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
     });
@@ -433,6 +479,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         DecodeArgs a = make_args(G, p, B, (const uint8_t*)dptr(r_syn), (const uint8_t*)dptr(r_base),
                                  (const uint8_t*)dptr(r_rd), (uint8_t*)dptr(r_x), (uint8_t*)dptr(r_corr), dptr(r_llr),
                                  (int32_t*)dptr(r_it), (uint8_t*)dptr(r_st), (int32_t*)dptr(r_ss), (uint8_t*)dptr(r_fl));
+        attach_queue(G, a);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         auto d2h = [&](void* h, const Reg& r, const char* what) {

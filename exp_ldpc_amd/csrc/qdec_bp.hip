@@ -1,31 +1,39 @@
-// qdec_bp.hip -- BP (+ small-set-flip) syndrome decoding on gfx950.
+// qdec_bp.hip -- BP + small-set-flip syndrome decoding on gfx950.
 //
-// One wave64 decodes one shot at a time (workgroup = one wave; the grid is
-// persistent and walks the shot range).  Everything a shot touches lives in that
-// wave's LDS slice:
-//   v2c  [m_pad][DRS]  variable->check messages, check-major, 16-B aligned rows
-//   c2v  [n_pad][DCS]  check->variable messages, variable-major
-//   xh   [n_pad+64]    hard decisions (u8; pad bytes stay 0)
-//   sres [m_pad]       residual syndrome for SSF
-// A lane owns checks i = lane + 64*rc and variables j = lane + 64*rv.  The check
-// pass reads its check's v2c row with ds_read_b128 (conflict-free strides,
-// qdec_internal.h lds_stride) and scatters c2v with ds_write_b32 through a slot
-// table held in registers; the variable pass does the mirror image.  Slot tables,
-// degrees and priors are loaded once per wave.
+// Two kernels per decode call:
 //
-// Arithmetic is the ldpc v1 bp_decoder restated operation for operation (see
-// oracle/bp_impl.inc, the CPU copy of the same loops): min-sum in the log domain
-// with alpha_t = 1 - 2^-t (ms_scaling_factor = 0) or a constant, product-sum in
-// the probability-ratio domain; row leave-one-out products/minima, column
-// prefix + suffix sums.  Built with -ffp-contract=off so every multiply and add is
-// separately rounded: results are bit-identical to the CPU oracle at the same
-// precision.  Min over a row uses min1/min2 (exactly the leave-one-out minimum).
+// 1. bp_wave_kernel: one wave64 decodes one shot at a time (workgroup = one
+//    wave; persistent grid walking the shot range).  Everything a shot touches
+//    lives in that wave's LDS slice:
+//      v2c  [m_pad][DRS]+64  variable->check messages, check-major, 16-B rows
+//      c2v  [n_pad][DCS]+64  check->variable messages, variable-major
+//      xh   [n_pad+64]       hard decisions (u8; the last 64 bytes stay 0)
+//    The trailing 64 elements of v2c/c2v are per-lane dummy slots: pad edges of a
+//    low-degree check/variable write there, so every scatter is unconditional and
+//    the passes are branch-free.  A lane owns checks i = lane + 64*rc and
+//    variables j = lane + 64*rv; the graph is padded to exactly RC*64 checks and
+//    RV*64 variables (QDEC_WAVE_SHAPES).  The check pass reads its row with
+//    ds_read_b128 (conflict-free strides, lds_stride) and scatters c2v through a
+//    slot table held in registers; the variable pass does the mirror image.
+//    With SSF requested, shots BP did not converge on are appended (hard
+//    decision + residual syndrome) to an HBM work queue instead of finalised.
+// 2. ssf_wave_kernel: one wave per queued shot runs small-set-flip and
+//    finalises it.  Only failing shots are touched (compacted), and the BP
+//    kernel's register budget does not carry the SSF scan.
+//
+// Arithmetic is the ldpc v1 bp_decoder restated (oracle/bp_impl.inc is the CPU
+// copy of the same loops): min-sum in the log domain with alpha_t = 1 - 2^-t
+// (ms_scaling_factor = 0) or a constant; product-sum in the probability-ratio
+// domain; column prefix + suffix sums in ldpc's order.  Built with
+// -ffp-contract=off so every multiply and add is rounded separately: results are
+// bit-identical to the CPU oracle at the same precision.
 //
 // Small-set-flip (build-defined spec): for each generator g (lane
-// owned), all subsets F of its <= 8 qubits are scored as
+// owned), every subset F of its <= 8 qubits is scored as
 //   key = (gain(F) * 840/|F|, -g, -F)      gain(F) = |s| - |s xor H 1_F|
 // with the syndrome restricted to the generator's <= 32 local checks as a bitmask
-// (popcount of xor with a per-subset mask).  A wave max picks the flip.
+// (popcount of xor with a per-subset mask: 5 VALU ops per subset).  A wave max
+// picks the flip.
 #include <hip/hip_runtime.h>
 
 #include "qdec_internal.h"
@@ -36,14 +44,12 @@ template <typename T>
 struct Big;
 template <>
 struct Big<float> {
-    static constexpr float v = 1e30f;   // fp32 stand-in for ldpc's 1e308 "no minimum yet"
+    static constexpr float v = 1e30f;  // fp32 stand-in for ldpc's 1e308 "no minimum yet"
 };
 template <>
 struct Big<double> {
     static constexpr double v = 1e308;
 };
-
-__constant__ int kInvSize[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
 
 // 16-byte LDS vector loads of D consecutive elements (16-B aligned).
 template <typename T, int D>
@@ -76,67 +82,107 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
     return v;
 }
 
+// median of three with lo <= hi: clamp(a, lo, hi) = min(hi, max(lo, a))
+__device__ __forceinline__ float med3(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
+__device__ __forceinline__ double med3(double a, double lo, double hi) { return fmin(hi, fmax(lo, a)); }
+
 template <typename T>
 __device__ __forceinline__ T alpha_at(int it, double ms_scaling) {
     return ms_scaling == 0.0 ? (T)(1.0 - ldexp(1.0, -it)) : (T)ms_scaling;
 }
 
-// Logical check: fail = any_r parity(lz[r] & (readout ^ corr)).  corr bits are
-// produced chunk by chunk (64 qubits) and ballot-ed into a wave-uniform word.
-constexpr int kMaxLogicalRounds = 4;  // k <= 256 in the wave kernels
+constexpr int kMaxLogicalRounds = 4;  // k <= 256 logicals in the fused check
 
-template <typename T, int METHOD, int RC, int RV>
+// 840/size for SSF subset sizes 1..8 (index 0 unused); read with uniform indices
+// (scalar loads).
+__constant__ int kInvSize[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
+
+// Final per-shot outputs from the hard decision in LDS: x_out, corr = base ^
+// fold(x), fail = any_r parity(lz[r] & (readout ^ corr)), status, ssf_steps.
+__device__ void finalize_shot(const DevGraph& g, const DecodeArgs& a, int64_t shot, const uint8_t* xh,
+                              bool conv, bool satisfied, int steps, int lane) {
+    const int n = g.n;
+    if (a.x_out)
+        for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    int lpar[kMaxLogicalRounds] = {0, 0, 0, 0};
+    if (a.corr_out || want_fail) {
+        for (int w0 = 0; w0 < g.lz_words; ++w0) {
+            const int q = w0 * 64 + lane;
+            int cb = 0;
+            if (q < g.n_data) {
+                cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
+                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+                if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+            }
+            if (want_fail) {
+                const int v = (q < g.n_data) ? ((a.readout[shot * g.n_data + q] ^ cb) & 1) : 0;
+                const unsigned long long word = __ballot(v);
+#pragma unroll
+                for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                    const int r = rr * 64 + lane;
+                    if (r < g.k) lpar[rr] ^= __popcll(g.lz[(size_t)r * g.lz_words + w0] & word) & 1;
+                }
+            }
+        }
+    }
+    int any_fail = 0;
+    if (want_fail) {
+        int f = 0;
+#pragma unroll
+        for (int rr = 0; rr < kMaxLogicalRounds; ++rr) f |= lpar[rr];
+        any_fail = __ballot(f) != 0ull;
+    }
+    if (lane == 0) {
+        if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
+        if (a.ssf_steps) a.ssf_steps[shot] = steps;
+        if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+    }
+}
+
+// ============================================================== BP kernel
+template <typename T, int METHOD, int RC, int RV, bool DEFER>
 __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
     constexpr int DRS = lds_stride<T, kDR>();
     constexpr int DCS = lds_stride<T, kDC>();
     constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* v2c = reinterpret_cast<T*>(smem);
-    T* c2v = v2c + g.m_pad * DRS;
-    uint8_t* xh = reinterpret_cast<uint8_t*>(c2v + g.n_pad * DCS);
-    uint8_t* sres = xh + g.n_pad + 64;
+    T* c2v = v2c + g.m_pad * DRS + 64;
+    uint8_t* xh = reinterpret_cast<uint8_t*>(c2v + g.n_pad * DCS + 64);
 
     const int lane = threadIdx.x;
     const SlotTables st = g.slots[PREC];
     const T* prior = reinterpret_cast<const T*>(g.prior[METHOD][PREC]);
     const int m = g.m, n = g.n;
 
-    // ---- per-lane graph tables (registers) ----
-    int degR[RC];
-    uint32_t rtab[RC][kDR];  // col | cslot << 16
-    int degC[RV];
+    // ---- per-lane graph tables (registers); pad edges -> dummy slots / zero bytes
+    uint32_t rtab[RC][kDR];      // col | cslot << 16
     uint32_t ctab[RV][kDC / 2];  // rslot pairs
     T L[RV];
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc) {
         const int i = rc * 64 + lane;
-        const bool on = rc * 64 < m;
-        degR[rc] = on ? g.r_deg[i] : 0;
 #pragma unroll
         for (int k = 0; k < kDR; ++k)
-            rtab[rc][k] = on ? ((uint32_t)g.r_col[k * g.m_pad + i] | ((uint32_t)st.r_cslot[k * g.m_pad + i] << 16))
-                             : (uint32_t)g.n_pad;
+            rtab[rc][k] = (uint32_t)g.r_col[k * g.m_pad + i] | ((uint32_t)st.r_cslot[k * g.m_pad + i] << 16);
     }
 #pragma unroll
     for (int rv = 0; rv < RV; ++rv) {
         const int j = rv * 64 + lane;
-        const bool on = rv * 64 < n;
-        degC[rv] = on ? g.c_deg[j] : 0;
-        L[rv] = on ? prior[j] : (T)0;
+        L[rv] = prior[j];
 #pragma unroll
         for (int k = 0; k < kDC / 2; ++k)
-            ctab[rv][k] = on ? ((uint32_t)st.c_rslot[(2 * k) * g.n_pad + j] |
-                                ((uint32_t)st.c_rslot[(2 * k + 1) * g.n_pad + j] << 16))
-                             : 0u;
+            ctab[rv][k] = (uint32_t)st.c_rslot[(2 * k) * g.n_pad + j] |
+                          ((uint32_t)st.c_rslot[(2 * k + 1) * g.n_pad + j] << 16);
     }
 
     // ---- one-time LDS init: pads hold neutral messages forever ----
     const T vneutral = METHOD == 1 ? Big<T>::v : (T)0;  // MS: |v| never the min; PS: factor 1
     const T cneutral = METHOD == 1 ? (T)0 : (T)1;       // MS: +0 in sums; PS: x1 in products
-    for (int e = lane; e < g.m_pad * DRS; e += 64) v2c[e] = vneutral;
-    for (int e = lane; e < g.n_pad * DCS; e += 64) c2v[e] = cneutral;
+    for (int e = lane; e < g.m_pad * DRS + 64; e += 64) v2c[e] = vneutral;
+    for (int e = lane; e < g.n_pad * DCS + 64; e += 64) c2v[e] = cneutral;
     for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
-    for (int e = lane; e < g.m_pad; e += 64) sres[e] = 0;
     __syncthreads();
 
     for (int64_t shot = blockIdx.x; shot < a.B; shot += gridDim.x) {
@@ -145,7 +191,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) {
             const int i = rc * 64 + lane;
-            sbit[rc] = (rc * 64 < m && i < m && a.syn) ? (a.syn[shot * m + i] & 1) : 0;
+            sbit[rc] = (i < m && a.syn) ? (a.syn[shot * m + i] & 1) : 0;
         }
         if (a.syn_flags) {
             const bool use_b = (a.syn_flags & 1) && a.base;
@@ -161,11 +207,9 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
             __syncthreads();
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
-                if (rc * 64 >= m) continue;
                 int p = 0;
 #pragma unroll
-                for (int k = 0; k < kDR; ++k)
-                    if (k < degR[rc]) p ^= xh[rtab[rc][k] & 0xffff];
+                for (int k = 0; k < kDR; ++k) p ^= xh[rtab[rc][k] & 0xffff];
                 sbit[rc] ^= p;
             }
             __syncthreads();
@@ -175,12 +219,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 #pragma unroll
         for (int rv = 0; rv < RV; ++rv) {
 #pragma unroll
-            for (int k = 0; k < kDC; ++k) {
-                if (k < degC[rv]) {
-                    const uint32_t s = (ctab[rv][k >> 1] >> ((k & 1) * 16)) & 0xffff;
-                    v2c[s] = L[rv];
-                }
-            }
+            for (int k = 0; k < kDC; ++k) v2c[(ctab[rv][k >> 1] >> ((k & 1) * 16)) & 0xffff] = L[rv];
         }
         __syncthreads();
 
@@ -193,32 +232,30 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
             const T alpha = alpha_at<T>(it, a.ms_scaling);
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
-                if (rc * 64 >= m) continue;
                 const int i = rc * 64 + lane;
                 T v[kDR];
                 lds_load<T, kDR>(v2c + i * DRS, v);
                 if constexpr (METHOD == 1) {
-                    T min1 = Big<T>::v, min2 = Big<T>::v;
-                    int idx = 0, par = sbit[rc];
+                    // ldpc's forward/backward leave-one-out minimum equals
+                    //   |c2v_k| = (|v_k| == m1) ? m2 : m1
+                    // with m1 <= m2 the two smallest |v| (ties: m2 = m1).  min/med3
+                    // give exactly that for NaN-free messages (priors in (0,1)).
+                    T m1 = Big<T>::v, m2 = Big<T>::v;
+                    bool par = sbit[rc] != 0;
+                    bool sk[kDR];
 #pragma unroll
                     for (int k = 0; k < kDR; ++k) {
                         const T av = fabs(v[k]);
-                        if (av < min1) {
-                            min2 = min1;
-                            min1 = av;
-                            idx = k;
-                        } else if (av < min2) {
-                            min2 = av;
-                        }
-                        par ^= (v[k] <= (T)0) ? 1 : 0;
+                        m2 = med3(av, m1, m2);
+                        m1 = fmin(m1, av);
+                        sk[k] = v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign
+                        par ^= sk[k];
                     }
+                    const T m1a = m1 * alpha, m2a = m2 * alpha;  // |c| * alpha, sign applied after
 #pragma unroll
                     for (int k = 0; k < kDR; ++k) {
-                        if (k < degR[rc]) {
-                            const T mag = (k == idx) ? min2 : min1;
-                            const int pk = par ^ ((v[k] <= (T)0) ? 1 : 0);
-                            c2v[rtab[rc][k] >> 16] = mag * (pk ? -alpha : alpha);
-                        }
+                        const T y = (fabs(v[k]) == m1) ? m2a : m1a;
+                        c2v[rtab[rc][k] >> 16] = (par ^ sk[k]) ? -y : y;
                     }
                 } else {
                     T t[kDR], fw[kDR];
@@ -235,7 +272,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
                         T c = fw[k] * b;
                         c = ((T)1 - c) / ((T)1 + c);
                         b *= t[k];
-                        if (k < degR[rc]) c2v[rtab[rc][k] >> 16] = c;
+                        c2v[rtab[rc][k] >> 16] = c;
                     }
                 }
             }
@@ -244,7 +281,6 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
             // ---- variable -> check, hard decision ----
 #pragma unroll
             for (int rv = 0; rv < RV; ++rv) {
-                if (rv * 64 >= n) continue;
                 const int j = rv * 64 + lane;
                 T c[kDC];
                 lds_load<T, kDC>(c2v + j * DCS, c);
@@ -264,7 +300,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
                     for (int k = kDC - 1; k >= 0; --k) {
                         const T out = pre[k] + suf;
                         suf += c[k];
-                        if (k < degC[rv]) v2c[(ctab[rv][k >> 1] >> ((k & 1) * 16)) & 0xffff] = out;
+                        v2c[(ctab[rv][k >> 1] >> ((k & 1) * 16)) & 0xffff] = out;  // pads -> dummy
                     }
                 } else {
                     T acc = L[rv];
@@ -282,10 +318,10 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
                         const T out = pre[k] * suf;
                         suf *= c[k];
                         if (isnan(suf)) suf = (T)1;
-                        if (k < degC[rv]) v2c[(ctab[rv][k >> 1] >> ((k & 1) * 16)) & 0xffff] = out;
+                        v2c[(ctab[rv][k >> 1] >> ((k & 1) * 16)) & 0xffff] = out;
                     }
                 }
-                if (j < n) xh[j] = (uint8_t)xb;
+                xh[j] = (uint8_t)xb;  // j in [n, n_pad): never read as data
             }
             __syncthreads();
 
@@ -294,11 +330,8 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
                 int p = sbit[rc];
-                if (rc * 64 < m) {
 #pragma unroll
-                    for (int k = 0; k < kDR; ++k)
-                        if (k < degR[rc]) p ^= xh[rtab[rc][k] & 0xffff];
-                }
+                for (int k = 0; k < kDR; ++k) p ^= xh[rtab[rc][k] & 0xffff];  // pads -> zero bytes
                 pres[rc] = p;
                 bad |= p;
             }
@@ -308,134 +341,148 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
             }
         }
         const int iters = conv ? it : a.max_iter;
-
-        // ---- small-set-flip on the residual syndrome ----
-        int steps = 0;
-        bool satisfied = conv;
-        if (a.ssf && !conv && g.n_gen > 0) {
-            int w_local = 0;
-#pragma unroll
-            for (int rc = 0; rc < RC; ++rc) {
-                const int i = rc * 64 + lane;
-                if (rc * 64 < m && i < m) sres[i] = (uint8_t)pres[rc];
-                w_local += pres[rc];
-            }
-            int sw = wave_sum_i32(w_local);
-            __syncthreads();
-            const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
-            while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
-                long long best = LLONG_MIN;
-                for (int g0 = 0; g0 < g.n_gen; g0 += 64) {
-                    const int gi = g0 + lane;
-                    if (gi >= g.n_gen) continue;
-                    const int w = g.g_w[gi];
-                    const int nlc = g.g_nlc[gi];
-                    uint32_t sl = 0;
-                    for (int c = 0; c < nlc; ++c) sl |= (uint32_t)sres[g.g_lc[c * g.g_pad + gi]] << c;
-                    uint32_t qm[kGenW];
-#pragma unroll
-                    for (int k = 0; k < kGenW; ++k) qm[k] = k < w ? g.g_qmask[k * g.g_pad + gi] : 0u;
-                    uint32_t lo[16];
-                    lo[0] = 0;
-#pragma unroll
-                    for (int l = 1; l < 16; ++l) {
-                        const int b = __builtin_ctz(l);
-                        lo[l] = lo[l & (l - 1)] ^ qm[b];
-                    }
-                    const int base = __builtin_popcount(sl);
-                    const int tlim = 1 << w;
-                    int best32 = INT_MIN;
-                    for (int hi = 0; hi < nhi; ++hi) {
-                        const uint32_t mh = ((hi & 1) ? qm[4] : 0u) ^ ((hi & 2) ? qm[5] : 0u) ^
-                                            ((hi & 4) ? qm[6] : 0u) ^ ((hi & 8) ? qm[7] : 0u);
-                        const uint32_t sh = sl ^ mh;
-                        const int hs = __builtin_popcount(hi);
-#pragma unroll
-                        for (int l = 0; l < 16; ++l) {
-                            const int t = hi * 16 + l;
-                            const int size = hs + __builtin_popcount(l);
-                            const int score = (base - __builtin_popcount(sh ^ lo[l])) * kInvSize[size];
-                            const int key = score * 256 + (255 - t);
-                            if (t > 0 && t < tlim) best32 = key > best32 ? key : best32;
-                        }
-                    }
-                    const long long key64 = ((long long)(best32 >> 8) << 32) |
-                                            ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);
-                    best = key64 > best ? key64 : best;
-                }
-                best = wave_max_i64(best);
-                const int score = (int)(best >> 32);
-                if (score <= 0) break;
-                const int gsel = 0xFFFFFF - (int)((best >> 8) & 0xFFFFFF);
-                const int tsel = 255 - (int)(best & 255);
-                const int size = __builtin_popcount(tsel);
-                const int gain = score * size / kSsfScale;
-                const int w = g.g_w[gsel];
-                uint32_t mask = 0;
-                for (int k = 0; k < w; ++k)
-                    if ((tsel >> k) & 1) mask ^= g.g_qmask[k * g.g_pad + gsel];
-                const int nlc = g.g_nlc[gsel];
-                if (lane < nlc && ((mask >> lane) & 1)) sres[g.g_lc[lane * g.g_pad + gsel]] ^= 1;
-                if (lane < w && ((tsel >> lane) & 1)) xh[g.g_q[lane * g.g_pad + gsel]] ^= 1;
-                __syncthreads();
-                sw -= gain;
-                ++steps;
-            }
-            satisfied = (sw == 0);
-            // leave sres clean for the next shot
-            for (int e = lane; e < g.m_pad; e += 64) sres[e] = 0;
-            __syncthreads();
-        }
-
-        // ---- outputs ----
-        if (a.x_out)
-            for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
+        if (lane == 0 && a.iters) a.iters[shot] = iters;
         if (a.llr_out) {
             T* lo = reinterpret_cast<T*>(a.llr_out);
 #pragma unroll
             for (int rv = 0; rv < RV; ++rv) {
                 const int j = rv * 64 + lane;
-                if (rv * 64 < n && j < n) {
+                if (j < n) {
                     if constexpr (METHOD == 1) lo[shot * n + j] = Q[rv];
                     else lo[shot * n + j] = (T)log((double)((T)1 / Q[rv]));
                 }
             }
         }
-        const bool want_fail = a.fail && a.readout && g.k > 0;
-        int lpar[kMaxLogicalRounds] = {0, 0, 0, 0};
-        if (a.corr_out || want_fail) {
-            for (int w0 = 0; w0 < g.lz_words; ++w0) {
-                const int q = w0 * 64 + lane;
-                int cb = 0;
-                if (q < g.n_data) {
-                    cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
-                    for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
-                    if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
-                }
-                if (want_fail) {
-                    const int v = (q < g.n_data) ? ((a.readout[shot * g.n_data + q] ^ cb) & 1) : 0;
-                    const unsigned long long word = __ballot(v);
+        if (DEFER && !conv) {
+            // hand the shot to the SSF kernel: hard decision + residual syndrome
+            int slot = 0;
+            if (lane == 0) slot = atomicAdd(a.q_count, 1);
+            slot = __shfl(slot, 0);
+            for (int j = lane; j < n; j += 64) a.q_x[(int64_t)slot * n + j] = xh[j];
 #pragma unroll
-                    for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
-                        const int r = rr * 64 + lane;
-                        if (r < g.k) lpar[rr] ^= __popcll(g.lz[(size_t)r * g.lz_words + w0] & word) & 1;
+            for (int rc = 0; rc < RC; ++rc) {
+                const int i = rc * 64 + lane;
+                if (i < m) a.q_r[(int64_t)slot * m + i] = (uint8_t)pres[rc];
+            }
+            if (lane == 0) a.q_idx[slot] = shot;
+        } else {
+            finalize_shot(g, a, shot, xh, conv, conv, 0, lane);
+        }
+        __syncthreads();
+    }
+}
+
+// ============================================================== SSF kernel
+template <int RG>
+__global__ __launch_bounds__(64) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint8_t* xh = smem;                // [n_pad + 64]
+    uint8_t* sres = xh + g.n_pad + 64;  // [m_pad + 64], last 64 bytes stay 0 (pad ids)
+    const int lane = threadIdx.x;
+    const int m = g.m, n = g.n;
+
+    // this lane's generators gi = rg*64 + lane: packed u8 local-check ids and
+    // per-qubit local-check masks (zero for qubits beyond the generator's weight)
+    uint32_t glc[RG][kGenLC / 4];
+    uint32_t gqm[RG][kGenW];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+        const int gi = rg * 64 + lane;
+#pragma unroll
+        for (int wq = 0; wq < kGenLC / 4; ++wq) glc[rg][wq] = g.g_lc8[wq * g.g_pad + gi];
+#pragma unroll
+        for (int k = 0; k < kGenW; ++k) gqm[rg][k] = g.g_qmask[k * g.g_pad + gi];
+    }
+    for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
+    for (int e = lane; e < g.m_pad + 64; e += 64) sres[e] = 0;
+    __syncthreads();
+
+    const int count = *a.q_count;
+    const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
+    const int nlcw = (g.g_nlcmax + 3) / 4;
+    for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+        const int64_t shot = a.q_idx[slot];
+        for (int j = lane; j < n; j += 64) xh[j] = a.q_x[(int64_t)slot * n + j];
+        int w_local = 0;
+        for (int i = lane; i < m; i += 64) {
+            const uint8_t r = a.q_r[(int64_t)slot * m + i];
+            sres[i] = r;
+            w_local += r;
+        }
+        int sw = wave_sum_i32(w_local);
+        __syncthreads();
+        int steps = 0;
+        while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
+            long long best = LLONG_MIN;
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg) {
+                const int gi = rg * 64 + lane;
+                uint32_t sl = 0;  // local syndrome of generator gi (pad ids -> zero bytes)
+#pragma unroll
+                for (int wq = 0; wq < kGenLC / 4; ++wq) {
+                    if (wq < nlcw) {
+                        const uint32_t pk = glc[rg][wq];
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb)
+                            sl |= (uint32_t)sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
                     }
                 }
-            }
-        }
-        int any_fail = 0;
-        if (want_fail) {
-            int f = 0;
+                if (__ballot(sl != 0u) == 0ull) continue;  // no positive gain in this round
+                const int base = __builtin_popcount(sl);
+                const uint32_t* qm = gqm[rg];
+                uint32_t lo[16];
+                lo[0] = 0;
 #pragma unroll
-            for (int rr = 0; rr < kMaxLogicalRounds; ++rr) f |= lpar[rr];
-            any_fail = __ballot(f) != 0ull;
+                for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
+                int best32 = INT_MIN;
+#pragma unroll 1
+                for (int hi = 0; hi < nhi; ++hi) {
+                    uint32_t mh = 0;
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb) mh ^= ((hi >> bb) & 1) ? qm[4 + bb] : 0u;
+                    const uint32_t sh = sl ^ mh;
+                    const int hs = __builtin_popcount(hi);
+                    int bh[5], ih[5];  // base*840/size and 840/size for size = hs + popc(l)
+#pragma unroll
+                    for (int d = 0; d < 5; ++d) {
+                        const int sz = hs + d;  // <= 8; uniform
+                        ih[d] = kInvSize[sz];
+                        bh[d] = sz > 0 ? base * ih[d] : INT_MIN / 512;
+                    }
+#pragma unroll
+                    for (int l = 0; l < 16; ++l) {
+                        const int d = __builtin_popcount(l);
+                        // score = gain * 840/|F|.  Subsets using qubits beyond the
+                        // generator's weight have zero masks: same gain, larger |F|,
+                        // never the maximum.  t = 0 scores INT_MIN/2 and never wins.
+                        const int score = bh[d] - __builtin_popcount(sh ^ lo[l]) * ih[d];
+                        const int t = hi * 16 + l;
+                        const int key = (int)(((unsigned)score << 8) | (unsigned)(255 - t));
+                        best32 = key > best32 ? key : best32;
+                    }
+                }
+                const long long key64 = ((long long)(best32 >> 8) << 32) |
+                                        ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);
+                best = key64 > best ? key64 : best;
+            }
+            best = wave_max_i64(best);
+            const int score = (int)(best >> 32);
+            if (score <= 0) break;
+            const int gsel = 0xFFFFFF - (int)((best >> 8) & 0xFFFFFF);
+            const int tsel = 255 - (int)(best & 255);
+            const int gain = score * __builtin_popcount(tsel) / kSsfScale;
+            const int w = g.g_w[gsel];
+            uint32_t mask = 0;
+            for (int k = 0; k < w; ++k)
+                if ((tsel >> k) & 1) mask ^= g.g_qmask[k * g.g_pad + gsel];
+            if (lane < g.g_nlc[gsel] && ((mask >> lane) & 1)) sres[g.g_lc[lane * g.g_pad + gsel]] ^= 1;
+            if (lane < w && ((tsel >> lane) & 1)) xh[g.g_q[lane * g.g_pad + gsel]] ^= 1;
+            __syncthreads();
+            sw -= gain;
+            ++steps;
         }
-        if (lane == 0) {
-            if (a.iters) a.iters[shot] = iters;
-            if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
-            if (a.ssf_steps) a.ssf_steps[shot] = steps;
-            if (a.fail) a.fail[shot] = (uint8_t)any_fail;
-        }
+        finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
+        for (int e = lane; e < g.m_pad; e += 64) sres[e] = 0;
         __syncthreads();
     }
 }
@@ -445,35 +492,57 @@ template <typename T>
 static size_t wave_lds_bytes(const DevGraph& g) {
     constexpr int DRS = lds_stride<T, kDR>();
     constexpr int DCS = lds_stride<T, kDC>();
-    return (size_t)g.m_pad * DRS * sizeof(T) + (size_t)g.n_pad * DCS * sizeof(T) + (size_t)g.n_pad + 64 +
-           (size_t)g.m_pad;
+    return ((size_t)g.m_pad * DRS + 64) * sizeof(T) + ((size_t)g.n_pad * DCS + 64) * sizeof(T) +
+           (size_t)g.n_pad + 64;
 }
 
-template <typename T, int METHOD, int RC, int RV>
-static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
-    auto kern = bp_wave_kernel<T, METHOD, RC, RV>;
-    const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
+template <typename K>
+static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
+                             const DecodeArgs& a) {
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
     long long grid = (long long)num_cus * per_cu;
-    if (grid > a.B) grid = a.B;
+    if (grid > work) grid = work;
     if (grid <= 0) return 0;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, stream, g, a);
     return (int)hipGetLastError();
 }
 
+template <typename T, int METHOD, int RC, int RV>
+static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
+    if (!a.ssf) return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, false>, lds, a.B, num_cus, stream, g, a);
+    if constexpr (RC > 2) {
+        return (int)hipErrorNotSupported;  // SSF tables cover m <= 128 in this build
+    } else {
+        if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+        hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
+        if (e != hipSuccess) return (int)e;
+        int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, true>, lds, a.B, num_cus, stream, g, a);
+        if (rc != 0) return rc;
+        const size_t lds2 = (size_t)g.n_pad + 64 + (size_t)g.m_pad + 64;
+        return launch_persistent(ssf_wave_kernel<RC>, (lds2 + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+    }
+}
+
 template <typename T, int METHOD>
 static int dispatch_shape(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     const int rc = g.m_pad / 64, rv = g.n_pad / 64;
-    if (rc <= 2 && rv <= 4) return launch_wave<T, METHOD, 2, 4>(g, a, num_cus, stream);
-    if (rc <= 4 && rv <= 9) return launch_wave<T, METHOD, 4, 9>(g, a, num_cus, stream);
+#define QDEC_SHAPE(R, V) \
+    if (rc == R && rv == V) return launch_wave<T, METHOD, R, V>(g, a, num_cus, stream);
+    QDEC_WAVE_SHAPES(QDEC_SHAPE)
+#undef QDEC_SHAPE
     return (int)hipErrorNotSupported;
 }
 
 bool wave_kernel_supports(const DevGraph& g) {
-    return g.max_rdeg <= kDR && g.max_cdeg <= kDC && g.m_pad / 64 <= 4 && g.n_pad / 64 <= 9 && g.k <= 256;
+    bool shape = false;
+#define QDEC_SHAPE(R, V) shape |= (g.m_pad == 64 * R && g.n_pad == 64 * V);
+    QDEC_WAVE_SHAPES(QDEC_SHAPE)
+#undef QDEC_SHAPE
+    return shape && g.max_rdeg <= kDR && g.max_cdeg <= kDC && g.k <= 256;
 }
 
 int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,

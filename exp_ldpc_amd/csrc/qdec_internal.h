@@ -13,6 +13,19 @@ constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
 constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
 constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
 
+// Wave-kernel shapes (check rounds RC, variable rounds RV): a graph is padded to
+// the first shape that holds it (RC*64 >= m, RV*64 >= n), and the kernel is
+// instantiated for exactly that shape so no per-round guard is needed.
+#define QDEC_WAVE_SHAPES(X) X(1, 2) X(2, 3) X(2, 4) X(2, 6) X(4, 9)
+inline bool pick_wave_shape(int m, int n, int* rc, int* rv) {
+    const int need_c = (m + 63) / 64, need_v = (n + 63) / 64;
+#define QDEC_PICK(R, V) \
+    if (need_c <= R && need_v <= V) { *rc = R; *rv = V; return true; }
+    QDEC_WAVE_SHAPES(QDEC_PICK)
+#undef QDEC_PICK
+    return false;
+}
+
 // LDS stride, in elements, of a per-lane block of D values of type T, chosen so a
 // wave reading its 64 blocks with 16-byte ds_read_b128 is bank-conflict free:
 // dword stride a multiple of 4 with an odd quotient (16 lanes cover 64 banks).
@@ -48,6 +61,8 @@ struct DevGraph {
     const uint16_t* g_q;          // [kGenW][g_pad]   qubit (column) k of generator g
     const uint8_t* g_nlc;         // [g_pad]
     const uint16_t* g_lc;         // [kGenLC][g_pad]  local check c of generator g
+    const uint32_t* g_lc8;        // [kGenLC/4][g_pad] the same ids packed 4 per word (pad -> m_pad)
+    int g_nlcmax;
     const uint32_t* g_qmask;      // [kGenW][g_pad]   local-check mask of qubit k
     // logicals (fused failure check)
     int k, lz_words;
@@ -68,6 +83,11 @@ struct DecodeArgs {
     uint8_t* status;
     int32_t* ssf_steps;
     uint8_t* fail;
+    // SSF work queue (device scratch owned by the graph handle)
+    int32_t* q_count;  // [1]
+    int64_t* q_idx;    // [B]   shot of queue slot
+    uint8_t* q_x;      // [B][n] BP hard decision
+    uint8_t* q_r;      // [B][m] residual syndrome
 };
 
 // Launchers (qdec_bp.hip / qdec_sample.hip).  Return hipError_t as int.

@@ -16,8 +16,9 @@ _i64 = C.c_int64
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    """(Re)build with make; a no-op when the library is up to date."""
+    cmd = ["make", "-C", HERE, "-s"] + (["-B"] if force else [])
+    subprocess.run(cmd, check=True)
     return LIB_PATH
 
 
@@ -32,7 +33,7 @@ class OracleLib:
         f.restype = _i32
         f.argtypes = [_i32, _i32, _p, _p, _p, _i32, _i32, _i32, C.c_double, _i32, _i32,
                       _i32, _p, _p, _i32, _i32, _i32, _p, _i64, _p, _p, _p, _i32,
-                      _p, _p, _p, _p, _p, _p, _p, _i32]
+                      _p, _p, _p, _p, _p, _p, _p, _i32, _i32]
         s = self.lib.qdo_sample_storage
         s.restype = _i32
         s.argtypes = [_i32, _i32, _p, _p, _i32, C.c_double, C.c_double, C.c_uint32, C.c_uint32,
@@ -46,7 +47,7 @@ class OracleLib:
 
     def decode(self, H, probs, syn=None, *, method="ms", precision="f64", max_iter=0, ms_scaling=0.0,
                ssf=False, ssf_max_steps=0, gens=None, n_data=None, fold_blocks=1, lz=None,
-               base=None, readout=None, syn_flags=0, B=None, want_llr=True, nthreads=0):
+               base=None, readout=None, syn_flags=0, B=None, want_llr=True, nthreads=0, ssf_impl="brute"):
         """Decode a batch; returns a dict of numpy arrays (same contract as
         exp_ldpc_amd.decoder.Decoder.decode_batch)."""
         import scipy.sparse as sp
@@ -89,7 +90,8 @@ class OracleLib:
                                        int(n_data), int(fold_blocks), k, _ptr(lz), int(B), _ptr(syn), _ptr(base),
                                        _ptr(readout), int(syn_flags), _ptr(out["x"]), _ptr(out["corr"]),
                                        _ptr(out["llr"]), _ptr(out["iters"]), _ptr(out["status"]),
-                                       _ptr(out["ssf_steps"]), _ptr(out["fail"]), int(nthreads))
+                                       _ptr(out["ssf_steps"]), _ptr(out["fail"]),
+                                       {"brute": 0, "fast": 1}[ssf_impl], int(nthreads))
         if rc != 0:
             raise ValueError(f"qdo_decode_batch failed with status {rc}")
         return out

@@ -114,6 +114,99 @@ static int ssf_run(const graph_t* g, int32_t n_gen, const int32_t* gen_ptr, cons
     return steps;
 }
 
+
+/* Same spec as ssf_run, evaluated with per-generator local-check bitmasks
+ * (popcount of s_local ^ M_F, subsets in ascending bitmask order).  Used for the
+ * timed CPU baseline; tests check it equals ssf_run bit for bit. */
+typedef struct {
+    int n_gen;
+    int* w;          /* [n_gen] */
+    int* nlc;        /* [n_gen] */
+    int* lc;         /* [n_gen][32] */
+    uint32_t* qm;    /* [n_gen][16] */
+    const int32_t* gen_ptr;
+    const int32_t* gen_idx;
+} ssf_tables_t;
+
+static int ssf_tables_build(const graph_t* g, int32_t n_gen, const int32_t* gen_ptr, const int32_t* gen_idx,
+                            ssf_tables_t* T) {
+    T->n_gen = n_gen;
+    T->gen_ptr = gen_ptr;
+    T->gen_idx = gen_idx;
+    T->w = (int*)calloc((size_t)n_gen, sizeof(int));
+    T->nlc = (int*)calloc((size_t)n_gen, sizeof(int));
+    T->lc = (int*)calloc((size_t)n_gen * 32, sizeof(int));
+    T->qm = (uint32_t*)calloc((size_t)n_gen * 16, sizeof(uint32_t));
+    if (!T->w || !T->nlc || !T->lc || !T->qm) return -1;
+    for (int gi = 0; gi < n_gen; ++gi) {
+        const int a = gen_ptr[gi], w = gen_ptr[gi + 1] - a;
+        if (w > 16) return -2;
+        T->w[gi] = w;
+        int* lc = T->lc + (size_t)gi * 32;
+        int nlc = 0;
+        for (int k = 0; k < w; ++k) {
+            const int q = gen_idx[a + k];
+            uint32_t mask = 0;
+            for (int u = g->col_ptr[q]; u < g->col_ptr[q + 1]; ++u) {
+                const int c = g->row_of[g->col_edge[u]];
+                int pos = -1;
+                for (int t = 0; t < nlc; ++t) if (lc[t] == c) { pos = t; break; }
+                if (pos < 0) {
+                    if (nlc >= 32) return -3;
+                    pos = nlc;
+                    lc[nlc++] = c;
+                }
+                mask ^= 1u << pos;
+            }
+            T->qm[(size_t)gi * 16 + k] = mask;
+        }
+        T->nlc[gi] = nlc;
+    }
+    return 0;
+}
+
+static void ssf_tables_free(ssf_tables_t* T) {
+    free(T->w); free(T->nlc); free(T->lc); free(T->qm);
+}
+
+static int ssf_run_fast(const graph_t* g, const ssf_tables_t* T, uint8_t* s, uint8_t* x, int max_steps,
+                        uint32_t* Mt) {
+    int steps = 0;
+    for (;;) {
+        if (max_steps > 0 && steps >= max_steps) break;
+        int bg = -1, bt = 0, bgain = 0, bsize = 1;
+        for (int gi = 0; gi < T->n_gen; ++gi) {
+            const int w = T->w[gi], nlc = T->nlc[gi];
+            const int* lc = T->lc + (size_t)gi * 32;
+            const uint32_t* qm = T->qm + (size_t)gi * 16;
+            uint32_t sl = 0;
+            for (int c = 0; c < nlc; ++c) sl |= (uint32_t)(s[lc[c]] & 1) << c;
+            const int base = __builtin_popcount(sl);
+            if (base == 0) continue; /* no subset can have positive gain */
+            Mt[0] = 0;
+            for (int t = 1; t < (1 << w); ++t) {
+                Mt[t] = Mt[t & (t - 1)] ^ qm[__builtin_ctz(t)];
+                const int gain = base - __builtin_popcount(sl ^ Mt[t]);
+                if (gain <= 0) continue;
+                const int size = __builtin_popcount(t);
+                if (bg < 0 || (long)gain * bsize > (long)bgain * size) {
+                    bg = gi; bt = t; bgain = gain; bsize = size;
+                }
+            }
+        }
+        if (bg < 0) break;
+        const int a = T->gen_ptr[bg], w = T->gen_ptr[bg + 1] - a;
+        for (int k = 0; k < w; ++k) {
+            if (!((bt >> k) & 1)) continue;
+            const int q = T->gen_idx[a + k];
+            x[q] ^= 1;
+            for (int u = g->col_ptr[q]; u < g->col_ptr[q + 1]; ++u) s[g->row_of[g->col_edge[u]]] ^= 1;
+        }
+        ++steps;
+    }
+    return steps;
+}
+
 /* ------------------------------------------------------------------ driver */
 int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx,
                      const double* channel_probs, int32_t method, int32_t precision,
@@ -126,7 +219,7 @@ int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t
                      int32_t syn_flags,
                      uint8_t* x_out, uint8_t* corr_out, double* llr_out,
                      int32_t* iters, uint8_t* status, int32_t* ssf_steps, uint8_t* fail,
-                     int32_t nthreads) {
+                     int32_t ssf_impl, int32_t nthreads) {
     if (m < 0 || n <= 0 || B < 0 || !row_ptr || !col_idx || !channel_probs) return -1;
     if (method != QDO_PRODUCT_SUM && method != QDO_MIN_SUM) return -2;
     if (ssf && (!gen_ptr || !gen_idx || n_gen <= 0)) return -3;
@@ -135,6 +228,12 @@ int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t
 
     graph_t g = {m, n, row_ptr, col_idx, NULL, NULL, NULL};
     if (build_csc(&g)) return -5;
+    ssf_tables_t st;
+    memset(&st, 0, sizeof(st));
+    if (ssf && ssf_impl == QDO_SSF_FAST && ssf_tables_build(&g, n_gen, gen_ptr, gen_idx, &st)) {
+        ssf_tables_free(&st);
+        return -6;
+    }
     const int E = row_ptr[m];
 
     double* llr64 = (double*)malloc(sizeof(double) * (size_t)n);
@@ -163,6 +262,7 @@ int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t
         uint8_t* corr = (uint8_t*)malloc((size_t)n_data);
         int* touched = (int*)malloc(sizeof(int) * (size_t)(m + 1));
         int* cnt = (int*)calloc((size_t)m + 1, sizeof(int));
+        uint32_t* Mt = (uint32_t*)malloc(sizeof(uint32_t) * 65536);
 
 #pragma omp for schedule(dynamic, 64)
         for (int64_t b = 0; b < B; ++b) {
@@ -197,7 +297,9 @@ int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t
             int steps = 0, satisfied = conv;
             if (ssf && !conv) {
                 for (int i = 0; i < m; ++i) hx[i] ^= s[i];
-                steps = ssf_run(&g, n_gen, gen_ptr, gen_idx, hx, x, ssf_max_steps, touched, cnt);
+                steps = (ssf_impl == QDO_SSF_FAST)
+                    ? ssf_run_fast(&g, &st, hx, x, ssf_max_steps, Mt)
+                    : ssf_run(&g, n_gen, gen_ptr, gen_idx, hx, x, ssf_max_steps, touched, cnt);
                 satisfied = 1;
                 for (int i = 0; i < m; ++i) if (hx[i]) { satisfied = 0; break; }
             }
@@ -226,9 +328,10 @@ int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t
             }
         }
         free(b2c64); free(c2b64); free(b2c32); free(c2b32); free(sg); free(lpr64); free(lpr32);
-        free(s); free(hx); free(x); free(corr); free(touched); free(cnt);
+        free(s); free(hx); free(x); free(corr); free(touched); free(cnt); free(Mt);
     }
     free(llr64); free(llr32);
+    if (ssf && ssf_impl == QDO_SSF_FAST) ssf_tables_free(&st);
     free(g.col_ptr); free(g.col_edge); free(g.row_of);
     return rc;
 }

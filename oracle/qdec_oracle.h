@@ -34,11 +34,14 @@ enum { QDO_PRODUCT_SUM = 0, QDO_MIN_SUM = 1 };
 enum { QDO_F64 = 0, QDO_F32 = 1 };
 enum { QDO_SYN_ADD_BASE = 1, QDO_SYN_ADD_READOUT = 2 };
 enum { QDO_ST_BP_CONVERGED = 1, QDO_ST_SATISFIED = 2 };
+enum { QDO_SSF_BRUTE = 0, QDO_SSF_FAST = 1 };
 
 /* Decode B shots (OpenMP over shots, nthreads <= 0 -> all cores).
  * See DESIGN.md "Decode contract" for the meaning of every argument; it is the
  * same contract as qd_decode_batch in include/qdec.h. llr_out is double for both
- * precisions (fp32 values are widened exactly). */
+ * precisions (fp32 values are widened exactly).  ssf_impl: QDO_SSF_BRUTE (the
+ * checker: literal subset enumeration) or QDO_SSF_FAST (same spec with bitmasks;
+ * the timed baseline). */
 int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx,
                      const double* channel_probs, int32_t method, int32_t precision,
                      int32_t max_iter, double ms_scaling,
@@ -50,7 +53,7 @@ int qdo_decode_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t
                      int32_t syn_flags,
                      uint8_t* x_out, uint8_t* corr_out, double* llr_out,
                      int32_t* iters, uint8_t* status, int32_t* ssf_steps, uint8_t* fail,
-                     int32_t nthreads);
+                     int32_t ssf_impl, int32_t nthreads);
 
 /* Storage-experiment sampler (DESIGN.md "Sampler"): Philox4x32-10, key =
  * {seed, stream}, counter = {word, event, shot_lo, shot_hi}.  Writes the
