@@ -63,6 +63,8 @@ SIGNATURES = {
     "qd_decode_batch_device": (_i32, [_p, C.POINTER(QdParams), _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "qd_sample_storage_device": (_i32, [_p, _i32, C.c_double, C.c_double, _u32, _u32, _i64, _i64, _p, _p, _p]),
     "qd_count_flags_device": (_i32, [_p, _i64, C.c_uint8, _p, _p]),
+    "qd_osd_batch": (_i32, [_i32, _i32, _p, _p, _i32, _i32, _i64, _p, _p, _p, _p, _i32]),
+    "qd_osd_last_error": (C.c_char_p, []),
 }
 
 

@@ -18,14 +18,14 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libqdec_hip.so")
-SOURCES = ["qdec_abi.cpp", "qdec_bp.hip", "qdec_sample.hip"]
-HEADERS = ["qdec_internal.h", os.path.join("..", "..", "include", "qdec.h")]
+SOURCES = ["qdec_abi.cpp", "qdec_osd.cpp", "qdec_bp.hip", "qdec_bp_block.hip", "qdec_sample.hip"]
+HEADERS = ["qdec_internal.h", "qdec_device.h", os.path.join("..", "..", "include", "qdec.h")]
 ARCH = os.environ.get("QDEC_OFFLOAD_ARCH", "gfx950")
 
 FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
-    "-Wall", "-Wno-unused-result",
+    "-Wall", "-Wno-unused-result", "-pthread",
 ]
 
 

@@ -213,7 +213,7 @@ def write_quantum_code(stream, code: QuantumCode) -> None:
                  f"{code.num_logicals}\n")
     for kind, mat in (("X", code.checks.x), ("Z", code.checks.z),
                       ("LZ", code.logicals.z), ("LX", code.logicals.x)):
-        csr = sp.csr_matrix(mat)
+        csr = sp.csr_matrix(mat, copy=True)
         csr.sum_duplicates()
         csr.sort_indices()
         csr.eliminate_zeros()

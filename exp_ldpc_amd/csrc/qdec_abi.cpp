@@ -84,6 +84,9 @@ struct qd_graph {
     // SSF work queue scratch (grow only): count | idx[B] | x[B][n] | r[B][m]
     void* qws = nullptr;
     int64_t q_cap = 0;
+    // HBM message scratch for the workgroup kernels on graphs too large for LDS
+    void* mws = nullptr;
+    size_t mws_bytes = 0;
 };
 
 namespace {
@@ -99,11 +102,6 @@ void build_tables(qd_graph* G, int m, int n) {
     DevGraph& g = G->dg;
     g.m = m;
     g.n = n;
-    int rc = 0, rv = 0;
-    if (!pick_wave_shape(m, n, &rc, &rv))
-        throw Fail(-21, "graph too large for this build's wave kernel (m <= 256, n <= 576)");
-    g.m_pad = rc * 64;
-    g.n_pad = rv * 64;
     const auto& rp = G->row_ptr;
     const auto& ci = G->col_idx;
     const int E = rp[m];
@@ -124,9 +122,29 @@ void build_tables(qd_graph* G, int m, int n) {
     for (int i = 0; i < m; ++i) g.max_rdeg = std::max(g.max_rdeg, rp[i + 1] - rp[i]);
     g.max_cdeg = 0;
     for (int j = 0; j < n; ++j) g.max_cdeg = std::max(g.max_cdeg, G->col_ptr[j + 1] - G->col_ptr[j]);
-    if (g.max_rdeg > kDR || g.max_cdeg > kDC)
-        throw Fail(-20, "graph degrees exceed this build's wave kernel (check degree <= 8, variable degree <= 4)");
-
+    g.E = E;
+    // CSC edge lists for the workgroup kernels
+    std::vector<int32_t> col_edge(std::max(E, 1), 0);
+    {
+        std::vector<int> f2(G->col_ptr.begin(), G->col_ptr.end() - 1);
+        for (int i = 0; i < m; ++i)
+            for (int e = rp[i]; e < rp[i + 1]; ++e) col_edge[f2[ci[e]]++] = e;
+    }
+    g.col_ptr = G->arena.upload(G->col_ptr);
+    g.col_edge = G->arena.upload(col_edge);
+    g.row_ptr = G->arena.upload(G->row_ptr);
+    g.col_idx = G->arena.upload(G->col_idx);
+    int rc = 0, rv = 0, drc = 0;
+    g.wave = (g.max_rdeg <= kDR && g.max_cdeg <= kDC && pick_wave_shape(m, n, g.max_rdeg, &rc, &rv, &drc)) ? 1 : 0;
+    if (!g.wave) {  // workgroup kernels: plain 64-padding, no wave tables
+        g.m_pad = (m + 63) / 64 * 64;
+        g.n_pad = (n + 63) / 64 * 64;
+        g.shape_drc = 0;
+        return;
+    }
+    g.m_pad = rc * 64;
+    g.n_pad = rv * 64;
+    g.shape_drc = drc;
     std::vector<uint8_t> r_deg(g.m_pad, 0), c_deg(g.n_pad, 0);
     // Pad edges (k >= degree, or padding rows/columns) point at per-lane dummies:
     // column n_pad + lane (a zero byte of xh) and message slot <array end> + lane.
@@ -194,6 +212,20 @@ void attach_queue(qd_graph* G, DecodeArgs& a) {
     a.q_idx = reinterpret_cast<int64_t*>(base + 256);
     a.q_x = base + 256 + (size_t)G->q_cap * 8;
     a.q_r = a.q_x + (size_t)G->q_cap * g.n;
+}
+
+void* message_scratch(qd_graph* G, int precision, size_t* bytes) {
+    const size_t need = block_scratch_bytes(G->dg, precision, G->num_cus);
+    *bytes = need;
+    if (need == 0) return nullptr;
+    if (need > G->mws_bytes) {
+        if (G->mws) hip_check(hipFree(G->mws), "hipFree scratch");
+        G->mws = nullptr;
+        G->mws_bytes = 0;
+        hip_check(hipMalloc(&G->mws, need), "hipMalloc message scratch");
+        G->mws_bytes = need;
+    }
+    return G->mws;
 }
 
 void check_graph(const qd_graph* g) {
@@ -304,6 +336,7 @@ int qd_graph_destroy(qd_graph* g) {
         g->prior_arena.release();
         if (g->ws) (void)hipFree(g->ws);
         if (g->qws) (void)hipFree(g->qws);
+        if (g->mws) (void)hipFree(g->mws);
         if (g->stream) (void)hipStreamDestroy(g->stream);
         delete g;
     });
@@ -315,9 +348,8 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         set_device(G);
         if (n_gen <= 0 || !gen_ptr || !gen_idx) throw Fail(-30, "invalid flip sets");
         DevGraph& g = G->dg;
-        if (g.m_pad > 128 || n_gen > g.m_pad)
-            throw Fail(-36, "SSF supports graphs with m <= 128 and at most m_pad generators in this build");
-        const int gp = g.m_pad;
+        const int gp = std::max(g.m_pad, (n_gen + 63) / 64 * 64);
+        const bool pack8 = g.m_pad <= 255;  // u8 local-check ids for the wave SSF kernel
         std::vector<uint8_t> w(gp, 0), nlc(gp, 0);
         std::vector<uint16_t> q((size_t)kGenW * gp, 0), lc((size_t)kGenLC * gp, 0);
         std::vector<uint32_t> qm((size_t)kGenW * gp, 0);
@@ -361,12 +393,13 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
             }
         }
         G->flip_arena.release();
+        g.g_lc8 = nullptr;
         g.g_w = G->flip_arena.upload(w);
         g.g_nlc = G->flip_arena.upload(nlc);
         g.g_q = G->flip_arena.upload(q);
         g.g_lc = G->flip_arena.upload(lc);
         g.g_qmask = G->flip_arena.upload(qm);
-        g.g_lc8 = G->flip_arena.upload(lc8);
+        if (pack8) g.g_lc8 = G->flip_arena.upload(lc8);
         g.g_nlcmax = nlcmax;
         g.n_gen = n_gen;
         g.g_pad = gp;
@@ -429,7 +462,9 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         set_device(G);
         DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
         attach_queue(G, a);
-        const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream);
+        size_t sb = 0;
+        void* scr = message_scratch(G, p->precision, &sb);
+        const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
     });
 }
@@ -480,7 +515,9 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
                                  (const uint8_t*)dptr(r_rd), (uint8_t*)dptr(r_x), (uint8_t*)dptr(r_corr), dptr(r_llr),
                                  (int32_t*)dptr(r_it), (uint8_t*)dptr(r_st), (int32_t*)dptr(r_ss), (uint8_t*)dptr(r_fl));
         attach_queue(G, a);
-        const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s);
+        size_t sb = 0;
+        void* scr = message_scratch(G, p->precision, &sb);
+        const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         auto d2h = [&](void* h, const Reg& r, const char* what) {
             if (h) hip_check(hipMemcpyAsync(h, dptr(r), r.bytes, hipMemcpyDeviceToHost, s), what);

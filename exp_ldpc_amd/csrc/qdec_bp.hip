@@ -36,66 +36,11 @@
 // picks the flip.
 #include <hip/hip_runtime.h>
 
-#include "qdec_internal.h"
+#include "qdec_device.h"
 
 namespace qdec {
 
-template <typename T>
-struct Big;
-template <>
-struct Big<float> {
-    static constexpr float v = 1e30f;  // fp32 stand-in for ldpc's 1e308 "no minimum yet"
-};
-template <>
-struct Big<double> {
-    static constexpr double v = 1e308;
-};
-
-// 16-byte LDS vector loads of D consecutive elements (16-B aligned).
-template <typename T, int D>
-__device__ __forceinline__ void lds_load(const T* p, T (&v)[D]) {
-    static_assert((D * sizeof(T)) % 16 == 0, "row must be a multiple of 16 bytes");
-    using V = __attribute__((ext_vector_type(16 / sizeof(T)))) T;
-    constexpr int per = 16 / sizeof(T);
-#pragma unroll
-    for (int c = 0; c < D / per; ++c) {
-        V x = *reinterpret_cast<const V*>(p + c * per);
-#pragma unroll
-        for (int e = 0; e < per; ++e) v[c * per + e] = x[e];
-    }
-}
-
-__device__ __forceinline__ long long wave_max_i64(long long v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        int lo = __shfl_xor((int)(unsigned)(v & 0xffffffffll), off);
-        int hi = __shfl_xor((int)(v >> 32), off);
-        long long o = ((long long)hi << 32) | (unsigned)lo;
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-__device__ __forceinline__ int wave_sum_i32(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-
-// median of three with lo <= hi: clamp(a, lo, hi) = min(hi, max(lo, a))
-__device__ __forceinline__ float med3(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
-__device__ __forceinline__ double med3(double a, double lo, double hi) { return fmin(hi, fmax(lo, a)); }
-
-template <typename T>
-__device__ __forceinline__ T alpha_at(int it, double ms_scaling) {
-    return ms_scaling == 0.0 ? (T)(1.0 - ldexp(1.0, -it)) : (T)ms_scaling;
-}
-
 constexpr int kMaxLogicalRounds = 4;  // k <= 256 logicals in the fused check
-
-// 840/size for SSF subset sizes 1..8 (index 0 unused); read with uniform indices
-// (scalar loads).
-__constant__ int kInvSize[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
 
 // Final per-shot outputs from the hard decision in LDS: x_out, corr = base ^
 // fold(x), fail = any_r parity(lz[r] & (readout ^ corr)), status, ssf_steps.
@@ -141,8 +86,9 @@ __device__ void finalize_shot(const DevGraph& g, const DecodeArgs& a, int64_t sh
 }
 
 // ============================================================== BP kernel
-template <typename T, int METHOD, int RC, int RV, bool DEFER>
+template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
 __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
+    static_assert(DRC <= kDR, "compute width exceeds the LDS row");
     constexpr int DRS = lds_stride<T, kDR>();
     constexpr int DCS = lds_stride<T, kDC>();
     constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
@@ -157,14 +103,14 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
     const int m = g.m, n = g.n;
 
     // ---- per-lane graph tables (registers); pad edges -> dummy slots / zero bytes
-    uint32_t rtab[RC][kDR];      // col | cslot << 16
+    uint32_t rtab[RC][DRC];      // col | cslot << 16 (slots >= DRC are pads: never used)
     uint32_t ctab[RV][kDC / 2];  // rslot pairs
     T L[RV];
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc) {
         const int i = rc * 64 + lane;
 #pragma unroll
-        for (int k = 0; k < kDR; ++k)
+        for (int k = 0; k < DRC; ++k)
             rtab[rc][k] = (uint32_t)g.r_col[k * g.m_pad + i] | ((uint32_t)st.r_cslot[k * g.m_pad + i] << 16);
     }
 #pragma unroll
@@ -209,7 +155,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
             for (int rc = 0; rc < RC; ++rc) {
                 int p = 0;
 #pragma unroll
-                for (int k = 0; k < kDR; ++k) p ^= xh[rtab[rc][k] & 0xffff];
+                for (int k = 0; k < DRC; ++k) p ^= xh[rtab[rc][k] & 0xffff];
                 sbit[rc] ^= p;
             }
             __syncthreads();
@@ -242,9 +188,9 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
                     // give exactly that for NaN-free messages (priors in (0,1)).
                     T m1 = Big<T>::v, m2 = Big<T>::v;
                     bool par = sbit[rc] != 0;
-                    bool sk[kDR];
+                    bool sk[DRC];
 #pragma unroll
-                    for (int k = 0; k < kDR; ++k) {
+                    for (int k = 0; k < DRC; ++k) {
                         const T av = fabs(v[k]);
                         m2 = med3(av, m1, m2);
                         m1 = fmin(m1, av);
@@ -253,22 +199,22 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
                     }
                     const T m1a = m1 * alpha, m2a = m2 * alpha;  // |c| * alpha, sign applied after
 #pragma unroll
-                    for (int k = 0; k < kDR; ++k) {
+                    for (int k = 0; k < DRC; ++k) {
                         const T y = (fabs(v[k]) == m1) ? m2a : m1a;
                         c2v[rtab[rc][k] >> 16] = (par ^ sk[k]) ? -y : y;
                     }
                 } else {
-                    T t[kDR], fw[kDR];
+                    T t[DRC], fw[DRC];
                     T f = sbit[rc] ? (T)-1 : (T)1;
 #pragma unroll
-                    for (int k = 0; k < kDR; ++k) {
+                    for (int k = 0; k < DRC; ++k) {
                         t[k] = (T)2 / ((T)1 + v[k]) - (T)1;
                         fw[k] = f;
                         f *= t[k];
                     }
                     T b = (T)1;
 #pragma unroll
-                    for (int k = kDR - 1; k >= 0; --k) {
+                    for (int k = DRC - 1; k >= 0; --k) {
                         T c = fw[k] * b;
                         c = ((T)1 - c) / ((T)1 + c);
                         b *= t[k];
@@ -331,7 +277,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
             for (int rc = 0; rc < RC; ++rc) {
                 int p = sbit[rc];
 #pragma unroll
-                for (int k = 0; k < kDR; ++k) p ^= xh[rtab[rc][k] & 0xffff];  // pads -> zero bytes
+                for (int k = 0; k < DRC; ++k) p ^= xh[rtab[rc][k] & 0xffff];  // pads -> zero bytes
                 pres[rc] = p;
                 bad |= p;
             }
@@ -374,7 +320,7 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 
 // ============================================================== SSF kernel
 template <int RG>
-__global__ __launch_bounds__(64) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64, 3) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint8_t* xh = smem;                // [n_pad + 64]
     uint8_t* sres = xh + g.n_pad + 64;  // [m_pad + 64], last 64 bytes stay 0 (pad ids)
@@ -428,42 +374,7 @@ __global__ __launch_bounds__(64) void ssf_wave_kernel(DevGraph g, DecodeArgs a) 
                     }
                 }
                 if (__ballot(sl != 0u) == 0ull) continue;  // no positive gain in this round
-                const int base = __builtin_popcount(sl);
-                const uint32_t* qm = gqm[rg];
-                uint32_t lo[16];
-                lo[0] = 0;
-#pragma unroll
-                for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
-                int best32 = INT_MIN;
-#pragma unroll 1
-                for (int hi = 0; hi < nhi; ++hi) {
-                    uint32_t mh = 0;
-#pragma unroll
-                    for (int bb = 0; bb < 4; ++bb) mh ^= ((hi >> bb) & 1) ? qm[4 + bb] : 0u;
-                    const uint32_t sh = sl ^ mh;
-                    const int hs = __builtin_popcount(hi);
-                    int bh[5], ih[5];  // base*840/size and 840/size for size = hs + popc(l)
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) {
-                        const int sz = hs + d;  // <= 8; uniform
-                        ih[d] = kInvSize[sz];
-                        bh[d] = sz > 0 ? base * ih[d] : INT_MIN / 512;
-                    }
-#pragma unroll
-                    for (int l = 0; l < 16; ++l) {
-                        const int d = __builtin_popcount(l);
-                        // score = gain * 840/|F|.  Subsets using qubits beyond the
-                        // generator's weight have zero masks: same gain, larger |F|,
-                        // never the maximum.  t = 0 scores INT_MIN/2 and never wins.
-                        const int score = bh[d] - __builtin_popcount(sh ^ lo[l]) * ih[d];
-                        const int t = hi * 16 + l;
-                        const int key = (int)(((unsigned)score << 8) | (unsigned)(255 - t));
-                        best32 = key > best32 ? key : best32;
-                    }
-                }
-                const long long key64 = ((long long)(best32 >> 8) << 32) |
-                                        ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);
-                best = key64 > best ? key64 : best;
+                best = max(best, gen_key64(gen_best_key(sl, gqm[rg], nhi), gi));
             }
             best = wave_max_i64(best);
             const int score = (int)(best >> 32);
@@ -510,28 +421,30 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
     return (int)hipGetLastError();
 }
 
-template <typename T, int METHOD, int RC, int RV>
+template <typename T, int METHOD, int RC, int RV, int DRC>
 static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
-    if (!a.ssf) return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, false>, lds, a.B, num_cus, stream, g, a);
-    if constexpr (RC > 2) {
-        return (int)hipErrorNotSupported;  // SSF tables cover m <= 128 in this build
-    } else {
-        if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
-        hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
-        if (e != hipSuccess) return (int)e;
-        int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, true>, lds, a.B, num_cus, stream, g, a);
-        if (rc != 0) return rc;
-        const size_t lds2 = (size_t)g.n_pad + 64 + (size_t)g.m_pad + 64;
-        return launch_persistent(ssf_wave_kernel<RC>, (lds2 + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+    if (!a.ssf)
+        return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, false>, lds, a.B, num_cus, stream, g, a);
+    if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, true>, lds, a.B, num_cus, stream, g, a);
+    if (rc != 0) return rc;
+    if constexpr (RC <= 2) {
+        if (g.n_gen <= g.m_pad && g.g_lc8) {  // register-cached tables: u8 ids, RC rounds of generators
+            const size_t lds2 = (size_t)g.n_pad + 64 + (size_t)g.m_pad + 64;
+            return launch_persistent(ssf_wave_kernel<RC>, (lds2 + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+        }
     }
+    return launch_ssf_block(g, a, num_cus, stream);
 }
 
 template <typename T, int METHOD>
 static int dispatch_shape(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     const int rc = g.m_pad / 64, rv = g.n_pad / 64;
-#define QDEC_SHAPE(R, V) \
-    if (rc == R && rv == V) return launch_wave<T, METHOD, R, V>(g, a, num_cus, stream);
+#define QDEC_SHAPE(R, V, D) \
+    if (rc == R && rv == V && g.shape_drc == D) return launch_wave<T, METHOD, R, V, D>(g, a, num_cus, stream);
     QDEC_WAVE_SHAPES(QDEC_SHAPE)
 #undef QDEC_SHAPE
     return (int)hipErrorNotSupported;
@@ -539,16 +452,17 @@ static int dispatch_shape(const DevGraph& g, const DecodeArgs& a, int num_cus, h
 
 bool wave_kernel_supports(const DevGraph& g) {
     bool shape = false;
-#define QDEC_SHAPE(R, V) shape |= (g.m_pad == 64 * R && g.n_pad == 64 * V);
+#define QDEC_SHAPE(R, V, D) shape |= (g.m_pad == 64 * R && g.n_pad == 64 * V && g.shape_drc == D);
     QDEC_WAVE_SHAPES(QDEC_SHAPE)
 #undef QDEC_SHAPE
     return shape && g.max_rdeg <= kDR && g.max_cdeg <= kDC && g.k <= 256;
 }
 
 int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
-                  hipStream_t stream) {
+                  hipStream_t stream, void* scratch, size_t scratch_bytes) {
     if (a.B <= 0) return 0;
-    if (!wave_kernel_supports(g)) return (int)hipErrorNotSupported;
+    if (!g.wave || !wave_kernel_supports(g))
+        return launch_decode_block(g, method, precision, a, num_cus, stream, scratch, scratch_bytes);
     if (precision == 1)
         return method == 1 ? dispatch_shape<float, 1>(g, a, num_cus, stream)
                            : dispatch_shape<float, 0>(g, a, num_cus, stream);

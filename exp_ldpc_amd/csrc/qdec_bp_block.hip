@@ -1,0 +1,390 @@
+// qdec_bp_block.hip -- BP + SSF for graphs outside the wave kernels' shapes
+// (multi-round spacetime matrices with R >= 2, codes with n > 576, degrees > 8/4).
+//
+// One 256-thread workgroup decodes one shot at a time (persistent grid).  Graph
+// tables are read from global memory (CSR row_ptr/col_idx, CSC col_ptr/col_edge;
+// L1/L2 resident, shared by every workgroup).  Messages are indexed by CSR edge
+// id: v2c[E], c2v[E] live in LDS when 2*E*sizeof(T) fits, otherwise in a
+// per-workgroup slice of an HBM scratch buffer (the HBM-bound regime of the 10k
+// and 50k qubit configurations).  The loops are ldpc v1's, operation for
+// operation (same arithmetic as the wave kernels and oracle/bp_impl.inc):
+//   check pass: thread per check, forward/backward along the row
+//   variable pass: thread per variable, prefix then suffix along the column
+// Small-set-flip runs in ssf_block_kernel on the same HBM work queue as the wave
+// path, with generators spread over the workgroup's threads.
+#include <hip/hip_runtime.h>
+
+#include "qdec_device.h"
+
+namespace qdec {
+
+constexpr int kBlock = 256;
+
+// Every block kernel starts its dynamic LDS with a 64-byte control area (no
+// static __shared__, so the dynamic base stays 16-byte aligned):
+//   [0, 32) long long red64[4]   [32, 48) int red32[4]   [48, 52) int slot
+constexpr int kCtrl = 64;
+
+// block-wide sum / max through the control area (all threads must call)
+__device__ long long block_max_i64(long long v, long long* red) {
+    v = wave_max_i64(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    long long r = red[0];
+    for (int i = 1; i < kBlock / 64; ++i) r = red[i] > r ? red[i] : r;
+    __syncthreads();
+    return r;
+}
+
+__device__ int block_sum_i32(int v, int* red) {
+    v = wave_sum_i32(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    int r = 0;
+    for (int i = 0; i < kBlock / 64; ++i) r += red[i];
+    __syncthreads();
+    return r;
+}
+
+// Outputs of one shot from its hard decision xh (LDS): x_out, corr = base ^
+// fold(xh), fail = any_r parity(lz[r] & (readout ^ corr)) (per-thread word parities
+// xor-reduced into LDS), status, ssf_steps.
+__device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t shot, const uint8_t* xh, bool conv,
+                               bool satisfied, int steps, int* lpar /* LDS [k] */) {
+    const int tid = threadIdx.x;
+    if (a.x_out)
+        for (int j = tid; j < g.n; j += kBlock) a.x_out[shot * g.n + j] = xh[j];
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    if (want_fail)
+        for (int r = tid; r < g.k; r += kBlock) lpar[r] = 0;
+    __syncthreads();
+    if (a.corr_out || want_fail) {
+        for (int w0 = tid; w0 < g.lz_words; w0 += kBlock) {
+            unsigned long long word = 0;
+            for (int b = 0; b < 64; ++b) {
+                const int q = w0 * 64 + b;
+                if (q >= g.n_data) break;
+                int cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
+                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+                if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+                if (want_fail) word |= (unsigned long long)((a.readout[shot * g.n_data + q] ^ cb) & 1) << b;
+            }
+            if (want_fail)
+                for (int r = 0; r < g.k; ++r)
+                    if (__popcll(g.lz[(size_t)r * g.lz_words + w0] & word) & 1) atomicXor(&lpar[r], 1);
+        }
+    }
+    __syncthreads();
+    int f = 0;
+    if (want_fail)
+        for (int r = tid; r < g.k; r += kBlock) f |= lpar[r];
+    f = __syncthreads_or(f);
+    if (tid == 0) {
+        if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
+        if (a.ssf_steps) a.ssf_steps[shot] = steps;
+        if (a.fail) a.fail[shot] = (uint8_t)(want_fail ? f : 0);
+    }
+    __syncthreads();
+}
+
+template <typename T, int METHOD, bool DEFER>
+__global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs a, T* gscratch, int msgs_in_lds) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int E = g.E, m = g.m, n = g.n, tid = threadIdx.x;
+    constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
+    int* slot_s = reinterpret_cast<int*>(smem + 48);
+    unsigned char* p = smem + kCtrl;
+    T* v2c;
+    if (msgs_in_lds) {
+        v2c = reinterpret_cast<T*>(p);
+        p += ((size_t)2 * E * sizeof(T) + 15) / 16 * 16;
+    } else {
+        v2c = gscratch + (size_t)blockIdx.x * 2 * E;
+    }
+    T* c2v = v2c + E;
+    uint8_t* xh = p;                      // [n_pad]
+    uint8_t* sb = xh + g.n_pad;           // [m_pad] syndrome bits
+    int* lpar = reinterpret_cast<int*>(sb + g.m_pad);  // [k]
+    uint8_t* rs = reinterpret_cast<uint8_t*>(lpar + (g.k > 0 ? g.k : 1));  // [m_pad] last residual
+    const T* prior = reinterpret_cast<const T*>(g.prior[METHOD][PREC]);
+    const int32_t* rp = g.row_ptr;
+    const int32_t* ci = g.col_idx;
+    const int32_t* cp = g.col_ptr;
+    const int32_t* ce = g.col_edge;
+
+    for (int64_t shot = blockIdx.x; shot < a.B; shot += gridDim.x) {
+        for (int i = tid; i < m; i += kBlock) {
+            int s = a.syn ? (a.syn[shot * m + i] & 1) : 0;
+            if (a.syn_flags) {
+                for (int e = rp[i]; e < rp[i + 1]; ++e) {
+                    const int j = ci[e];
+                    if (j >= g.n_data) continue;
+                    if ((a.syn_flags & 1) && a.base) s ^= a.base[shot * g.n_data + j] & 1;
+                    if ((a.syn_flags & 2) && a.readout) s ^= a.readout[shot * g.n_data + j] & 1;
+                }
+            }
+            sb[i] = (uint8_t)s;
+        }
+        for (int j = tid; j < n; j += kBlock)
+            for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[ce[t]] = prior[j];
+        __syncthreads();
+        int it = 1;
+        bool conv = false;
+        for (; it <= a.max_iter; ++it) {
+            const T alpha = alpha_at<T>(it, a.ms_scaling);
+            for (int i = tid; i < m; i += kBlock) {
+                const int e0 = rp[i], e1 = rp[i + 1];
+                if constexpr (METHOD == 1) {
+                    T m1 = Big<T>::v, m2 = Big<T>::v;
+                    int par = sb[i];
+                    for (int e = e0; e < e1; ++e) {
+                        const T v = v2c[e];
+                        const T av = fabs(v);
+                        m2 = med3(av, m1, m2);
+                        m1 = fmin(m1, av);
+                        par ^= v <= (T)0;
+                    }
+                    const T m1a = m1 * alpha, m2a = m2 * alpha;
+                    for (int e = e0; e < e1; ++e) {
+                        const T v = v2c[e];
+                        const T y = (fabs(v) == m1) ? m2a : m1a;
+                        c2v[e] = (par ^ (v <= (T)0)) ? -y : y;
+                    }
+                } else {
+                    T f = sb[i] ? (T)-1 : (T)1;
+                    for (int e = e0; e < e1; ++e) {
+                        c2v[e] = f;
+                        f *= (T)2 / ((T)1 + v2c[e]) - (T)1;
+                    }
+                    T b = (T)1;
+                    for (int e = e1 - 1; e >= e0; --e) {
+                        T c = c2v[e] * b;
+                        c2v[e] = ((T)1 - c) / ((T)1 + c);
+                        b *= (T)2 / ((T)1 + v2c[e]) - (T)1;
+                    }
+                }
+            }
+            __syncthreads();
+            for (int j = tid; j < n; j += kBlock) {
+                const int t0 = cp[j], t1 = cp[j + 1];
+                T acc = prior[j];
+                if constexpr (METHOD == 1) {
+                    for (int t = t0; t < t1; ++t) {
+                        const int e = ce[t];
+                        v2c[e] = acc;
+                        acc += c2v[e];
+                    }
+                    xh[j] = acc <= (T)0;
+                    T suf = (T)0;
+                    for (int t = t1 - 1; t >= t0; --t) {
+                        const int e = ce[t];
+                        v2c[e] = v2c[e] + suf;
+                        suf += c2v[e];
+                    }
+                } else {
+                    for (int t = t0; t < t1; ++t) {
+                        const int e = ce[t];
+                        v2c[e] = acc;
+                        acc *= c2v[e];
+                        if (isnan(acc)) acc = (T)1;
+                    }
+                    xh[j] = acc >= (T)1;
+                    T suf = (T)1;
+                    for (int t = t1 - 1; t >= t0; --t) {
+                        const int e = ce[t];
+                        v2c[e] = v2c[e] * suf;
+                        suf *= c2v[e];
+                        if (isnan(suf)) suf = (T)1;
+                    }
+                }
+            }
+            __syncthreads();
+            int bad = 0;
+            for (int i = tid; i < m; i += kBlock) {
+                int par = sb[i];
+                for (int e = rp[i]; e < rp[i + 1]; ++e) par ^= xh[ci[e]];
+                rs[i] = (uint8_t)par;
+                bad |= par;
+            }
+            if (!__syncthreads_or(bad)) {
+                conv = true;
+                break;
+            }
+        }
+        const int iters = conv ? it : a.max_iter;
+        if (tid == 0 && a.iters) a.iters[shot] = iters;
+        if (a.llr_out) {  // soft output of the last iteration, same summation order
+            T* lo = reinterpret_cast<T*>(a.llr_out);
+            for (int j = tid; j < n; j += kBlock) {
+                T acc = prior[j];
+                for (int t = cp[j]; t < cp[j + 1]; ++t) {
+                    if constexpr (METHOD == 1) {
+                        acc += c2v[ce[t]];
+                    } else {
+                        acc *= c2v[ce[t]];
+                        if (isnan(acc)) acc = (T)1;
+                    }
+                }
+                if constexpr (METHOD == 1) lo[shot * n + j] = acc;
+                else lo[shot * n + j] = (T)log((double)((T)1 / acc));
+            }
+        }
+        if (DEFER && !conv) {
+            if (tid == 0) *slot_s = atomicAdd(a.q_count, 1);
+            __syncthreads();
+            const int slot = *slot_s;
+            for (int j = tid; j < n; j += kBlock) a.q_x[(int64_t)slot * n + j] = xh[j];
+            for (int i = tid; i < m; i += kBlock) a.q_r[(int64_t)slot * m + i] = rs[i];
+            if (tid == 0) a.q_idx[slot] = shot;
+            __syncthreads();
+        } else {
+            finalize_block(g, a, shot, xh, conv, conv, 0, lpar);
+        }
+    }
+}
+
+// Small-set-flip for queued shots, one workgroup per shot; generator gi is
+// scanned by thread gi % 256.  Same keys as ssf_wave_kernel.
+__global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    long long* redl = reinterpret_cast<long long*>(smem);
+    int* redi = reinterpret_cast<int*>(smem + 32);
+    uint8_t* xh = smem + kCtrl;       // [n_pad]
+    uint8_t* sres = xh + g.n_pad;     // [m_pad]
+    int* lpar = reinterpret_cast<int*>(sres + g.m_pad);  // [k]
+    const int tid = threadIdx.x, m = g.m, n = g.n;
+    const int count = *a.q_count;
+    const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
+    for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+        const int64_t shot = a.q_idx[slot];
+        for (int j = tid; j < n; j += kBlock) xh[j] = a.q_x[(int64_t)slot * n + j];
+        int wl = 0;
+        for (int i = tid; i < m; i += kBlock) {
+            const uint8_t r = a.q_r[(int64_t)slot * m + i];
+            sres[i] = r;
+            wl += r;
+        }
+        int sw = block_sum_i32(wl, redi);  // includes a barrier: LDS fills visible
+        int steps = 0;
+        while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
+            long long best = LLONG_MIN;
+            for (int gi = tid; gi < g.n_gen; gi += kBlock) {
+                const int nlc = g.g_nlc[gi];
+                uint32_t sl = 0;
+                for (int c = 0; c < nlc; ++c) sl |= (uint32_t)sres[g.g_lc[c * g.g_pad + gi]] << c;
+                if (sl == 0) continue;
+                uint32_t qm[kGenW];
+#pragma unroll
+                for (int k = 0; k < kGenW; ++k) qm[k] = g.g_qmask[k * g.g_pad + gi];
+                best = max(best, gen_key64(gen_best_key(sl, qm, nhi), gi));
+            }
+            best = block_max_i64(best, redl);
+            const int score = (int)(best >> 32);
+            if (best == LLONG_MIN || score <= 0) break;
+            const int gsel = 0xFFFFFF - (int)((best >> 8) & 0xFFFFFF);
+            const int tsel = 255 - (int)(best & 255);
+            const int gain = score * __builtin_popcount(tsel) / kSsfScale;
+            const int w = g.g_w[gsel];
+            uint32_t mask = 0;
+            for (int k = 0; k < w; ++k)
+                if ((tsel >> k) & 1) mask ^= g.g_qmask[k * g.g_pad + gsel];
+            if (tid < g.g_nlc[gsel] && ((mask >> tid) & 1)) sres[g.g_lc[tid * g.g_pad + gsel]] ^= 1;
+            if (tid < w && ((tsel >> tid) & 1)) xh[g.g_q[tid * g.g_pad + gsel]] ^= 1;
+            __syncthreads();
+            sw -= gain;
+            ++steps;
+        }
+        finalize_block(g, a, shot, xh, false, sw == 0, steps, lpar);
+    }
+}
+
+// ---------------------------------------------------------------- launcher
+template <typename K, typename P>
+static int launch_block(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, int cap_per_cu,
+                        const DevGraph& g, const DecodeArgs& a, P* extra0, int extra1) {
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, lds);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    if (cap_per_cu > 0 && per_cu > cap_per_cu) per_cu = cap_per_cu;
+    long long grid = (long long)num_cus * per_cu;
+    if (grid > work) grid = work;
+    if (grid <= 0) return 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, stream, g, a, extra0, extra1);
+    return (int)hipGetLastError();
+}
+
+template <typename K>
+static int launch_block2(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
+                         const DecodeArgs& a) {
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, lds);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    long long grid = (long long)num_cus * per_cu;
+    if (grid > work) grid = work;
+    if (grid <= 0) return 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, stream, g, a);
+    return (int)hipGetLastError();
+}
+
+// control area + xh + one or two m_pad byte arrays + logical parities
+size_t block_small_lds(const DevGraph& g) {
+    return kCtrl + (size_t)g.n_pad + 2 * (size_t)g.m_pad + 4 * (size_t)(g.k > 0 ? g.k : 1);
+}
+
+constexpr size_t kLdsMsgLimit = 64 * 1024;  // messages in LDS up to this (2 workgroups per CU)
+
+template <typename T, int METHOD>
+static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, void* scratch,
+                              size_t scratch_bytes) {
+    const size_t msg = ((size_t)2 * g.E * sizeof(T) + 15) / 16 * 16;
+    const size_t small = (block_small_lds(g) + 15) / 16 * 16;
+    const bool in_lds = msg + small <= kLdsMsgLimit;
+    const size_t lds = small + (in_lds ? msg : 0);
+    int cap = 0;
+    if (!in_lds) {
+        // per-workgroup message slices in HBM scratch
+        const size_t per_wg = (size_t)2 * g.E * sizeof(T);
+        if (!scratch || per_wg == 0) return (int)hipErrorInvalidValue;
+        const long long max_wg = (long long)(scratch_bytes / per_wg);
+        if (max_wg < 1) return (int)hipErrorOutOfMemory;
+        cap = (int)std::max<long long>(1, max_wg / num_cus);
+    }
+    T* gs = reinterpret_cast<T*>(scratch);
+    if (!a.ssf)
+        return launch_block(bp_block_kernel<T, METHOD, false>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+    if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    int rc = launch_block(bp_block_kernel<T, METHOD, true>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+    if (rc != 0) return rc;
+    return launch_block2(ssf_block_kernel, small, a.B, num_cus, stream, g, a);
+}
+
+size_t block_scratch_bytes(const DevGraph& g, int precision, int num_cus) {
+    const size_t tsz = precision == 1 ? 4 : 8;
+    const size_t msg = ((size_t)2 * g.E * tsz + 15) / 16 * 16;
+    const size_t small = (block_small_lds(g) + 15) / 16 * 16;
+    if (msg + small <= kLdsMsgLimit) return 0;
+    return (size_t)num_cus * 4 * (size_t)2 * g.E * tsz;  // up to 4 workgroups per CU
+}
+
+int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
+                        hipStream_t stream, void* scratch, size_t scratch_bytes) {
+    if (a.B <= 0) return 0;
+    if (a.ssf && g.n_gen <= 0) return (int)hipErrorInvalidValue;
+    if (precision == 1)
+        return method == 1 ? launch_block_typed<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
+                           : launch_block_typed<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
+    return method == 1 ? launch_block_typed<double, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
+                       : launch_block_typed<double, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
+}
+
+int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    return launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+}
+
+}  // namespace qdec

@@ -1,0 +1,107 @@
+// qdec_device.h -- device helpers shared by the wave kernels (qdec_bp.hip) and
+// the workgroup kernels (qdec_bp_block.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "qdec_internal.h"
+
+namespace qdec {
+
+template <typename T>
+struct Big;
+template <>
+struct Big<float> {
+    static constexpr float v = 1e30f;  // fp32 stand-in for ldpc's 1e308 "no minimum yet"
+};
+template <>
+struct Big<double> {
+    static constexpr double v = 1e308;
+};
+
+// 16-byte LDS vector loads of D consecutive elements (16-B aligned).
+template <typename T, int D>
+__device__ __forceinline__ void lds_load(const T* p, T (&v)[D]) {
+    static_assert((D * sizeof(T)) % 16 == 0, "row must be a multiple of 16 bytes");
+    using V = __attribute__((ext_vector_type(16 / sizeof(T)))) T;
+    constexpr int per = 16 / sizeof(T);
+#pragma unroll
+    for (int c = 0; c < D / per; ++c) {
+        V x = *reinterpret_cast<const V*>(p + c * per);
+#pragma unroll
+        for (int e = 0; e < per; ++e) v[c * per + e] = x[e];
+    }
+}
+
+__device__ __forceinline__ long long wave_max_i64(long long v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        int lo = __shfl_xor((int)(unsigned)(v & 0xffffffffll), off);
+        int hi = __shfl_xor((int)(v >> 32), off);
+        long long o = ((long long)hi << 32) | (unsigned)lo;
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// median of three with lo <= hi: clamp(a, lo, hi) = min(hi, max(lo, a))
+__device__ __forceinline__ float med3(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
+__device__ __forceinline__ double med3(double a, double lo, double hi) { return fmin(hi, fmax(lo, a)); }
+
+template <typename T>
+__device__ __forceinline__ T alpha_at(int it, double ms_scaling) {
+    return ms_scaling == 0.0 ? (T)(1.0 - ldexp(1.0, -it)) : (T)ms_scaling;
+}
+
+// 840/size for SSF subset sizes 1..8 (index 0 unused); read with uniform indices
+// (scalar loads).
+static __constant__ int kInvSize[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
+
+
+// Best small-set-flip key of one generator: all subsets t of its <= 8 qubits,
+// key32 = (gain * 840/|t|) << 8 | (255 - t), where gain = popc(sl) -
+// popc(sl ^ M_t), M_t = xor of the qubits' local-check masks qm.  Subsets using
+// qubits beyond the generator's weight have zero masks (same gain, larger |t|),
+// so they never win; t = 0 scores 0 and is never selected (a flip needs a
+// positive score).  5 VALU ops per subset; nhi = 2^(wmax-4) blocks of 16.
+__device__ __forceinline__ int gen_best_key(uint32_t sl, const uint32_t (&qm)[kGenW], int nhi) {
+    const int base = __builtin_popcount(sl);
+    uint32_t lo[16];
+    lo[0] = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
+    int best32 = INT_MIN;
+#pragma unroll 1
+    for (int hi = 0; hi < nhi; ++hi) {
+        uint32_t mh = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) mh ^= ((hi >> bb) & 1) ? qm[4 + bb] : 0u;
+        const uint32_t sh = sl ^ mh;
+        const int hs = __builtin_popcount(hi);
+        int ih[5];  // 840/size for size = hs + popc(l)
+#pragma unroll
+        for (int d = 0; d < 5; ++d) ih[d] = kInvSize[hs + d];  // uniform scalar loads
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            const int d = __builtin_popcount(l);
+            // full-rate 24-bit multiply (|base - cnt| <= 32, ih <= 840)
+            const int score = __mul24(base - (int)__builtin_popcount(sh ^ lo[l]), ih[d]);
+            const int t = hi * 16 + l;
+            const int key = (int)(((unsigned)score << 8) | (unsigned)(255 - t));
+            best32 = key > best32 ? key : best32;
+        }
+    }
+    return best32;
+}
+
+// (score, -g, -t) packed so that a signed max picks the spec's winner.
+__device__ __forceinline__ long long gen_key64(int best32, int gi) {
+    return ((long long)(best32 >> 8) << 32) | ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);
+}
+
+}  // namespace qdec

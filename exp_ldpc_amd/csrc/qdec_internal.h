@@ -13,14 +13,15 @@ constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
 constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
 constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
 
-// Wave-kernel shapes (check rounds RC, variable rounds RV): a graph is padded to
-// the first shape that holds it (RC*64 >= m, RV*64 >= n), and the kernel is
-// instantiated for exactly that shape so no per-round guard is needed.
-#define QDEC_WAVE_SHAPES(X) X(1, 2) X(2, 3) X(2, 4) X(2, 6) X(4, 9)
-inline bool pick_wave_shape(int m, int n, int* rc, int* rv) {
+// Wave-kernel shapes (check rounds RC, variable rounds RV, check-node compute
+// width D <= kDR): a graph is padded to the first shape that holds it (RC*64 >= m,
+// RV*64 >= n, D >= max check degree), and the kernel is instantiated for exactly
+// that shape so no per-round guard is needed.  (2, 4, 7) is the n = 225 HGP code.
+#define QDEC_WAVE_SHAPES(X) X(1, 2, 8) X(2, 3, 6) X(2, 3, 8) X(2, 4, 7) X(2, 4, 8) X(2, 6, 8) X(4, 9, 8)
+inline bool pick_wave_shape(int m, int n, int max_rdeg, int* rc, int* rv, int* drc) {
     const int need_c = (m + 63) / 64, need_v = (n + 63) / 64;
-#define QDEC_PICK(R, V) \
-    if (need_c <= R && need_v <= V) { *rc = R; *rv = V; return true; }
+#define QDEC_PICK(R, V, D) \
+    if (need_c <= R && need_v <= V && max_rdeg <= D) { *rc = R; *rv = V; *drc = D; return true; }
     QDEC_WAVE_SHAPES(QDEC_PICK)
 #undef QDEC_PICK
     return false;
@@ -45,16 +46,21 @@ struct SlotTables {
 
 struct DevGraph {
     int m, n, m_pad, n_pad;       // pads: multiples of 64
+    int E;                        // edges (nnz of H)
+    int wave;                     // 1: a wave-kernel shape holds this graph
     int n_data, fold_blocks;
     int max_rdeg, max_cdeg;
+    int shape_drc;                // check-node compute width of the chosen wave shape
     const uint8_t* r_deg;         // [m_pad]
     const uint16_t* r_col;        // [kDR][m_pad]  column of edge k of check i (pad -> n_pad)
     const uint8_t* c_deg;         // [n_pad]
     SlotTables slots[2];          // [QD_F64], [QD_F32]
     const void* prior[2][2];      // [method][precision] initial message per column, [n_pad]
-    // CSR copy (sampler; generic paths)
+    // CSR / CSC copies (sampler; workgroup kernels)
     const int32_t* row_ptr;
     const int32_t* col_idx;
+    const int32_t* col_ptr;       // [n+1]
+    const int32_t* col_edge;      // [E] CSR edge ids of column j, ascending row
     // flip sets (SSF)
     int n_gen, g_pad, g_wmax;
     const uint8_t* g_w;           // [g_pad]
@@ -92,7 +98,11 @@ struct DecodeArgs {
 
 // Launchers (qdec_bp.hip / qdec_sample.hip).  Return hipError_t as int.
 int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a,
-                  int num_cus, hipStream_t stream);
+                  int num_cus, hipStream_t stream, void* scratch, size_t scratch_bytes);
+int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
+                        hipStream_t stream, void* scratch, size_t scratch_bytes);
+int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream);
+size_t block_scratch_bytes(const DevGraph& g, int precision, int num_cus);
 int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,
                           uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
                           uint8_t* syn, uint8_t* readout, int num_cus, hipStream_t stream);

@@ -1,0 +1,448 @@
+"""Batched storage-experiment harness: decoder modes, run_simulation, p_sweep.
+
+Mirrors ``python/qldpc/misc/_experiment.py`` and ``python/qldpc/misc/p_sweep.py``
+with the per-shot Python loop (``_experiment.py:200-209``) replaced by batched
+device pipelines: shots are sampled on the GPU (storage_sim.StorageSim.
+sample_device), decoded by libqdec_hip.so and reduced to failure counts on the
+device.  Decoder modes (``--decoder_mode``):
+
+  bposd              BP(+OSD) on the spacetime matrix, fold     (_experiment.py:62-83)
+  bposd_hybrid       BP on spacetime, fold, then BP+OSD on H     (_experiment.py:85-126)
+  bposd_single_shot  per-round [H|I] BP+OSD, then BP+OSD on H    (_experiment.py:12-60)
+  bpssf              BP + small-set-flip on H (R = 0); R >= 1 runs bpssf_hybrid
+  bpssf_hybrid       BP on spacetime, fold, then BP+SSF on H     (build-defined)
+  bp                 BP only on the spacetime matrix
+  bpd_detector       not supported (needs a Stim detector error model)
+
+OSD runs on the host cores for the shots BP did not converge on (osd.py).
+Logical failure = any(Lz (readout + correction)) mod 2 as at _experiment.py:209
+(computed in-kernel for device stages).
+"""
+from __future__ import annotations
+
+import math
+import os
+import re
+import sys
+import time
+from argparse import ArgumentParser
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Callable, Dict, Tuple
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _abi
+from .codes import read_quantum_code
+from .decoder import Decoder
+from .osd import OsdSolver
+from .spacetime import SpacetimeCode, SpacetimeCodeSingleShot
+from .storage_sim import build_storage_simulation
+
+__all__ = ["DECODER_MODES", "BatchPipeline", "BPOSDCorrect", "BPOSDHybridCorrect", "BPOSDCorrectSingleShot",
+           "BPSSFCorrect", "run_simulation", "add_bposd_args", "unpack_bposd_args", "load_code", "p_sweep",
+           "p_sweep_main", "parse_sweep_spec"]
+
+DECODER_MODES = ["bposd", "bposd_single_shot", "bposd_hybrid", "bpd_detector", "bpssf", "bpssf_hybrid", "bp"]
+DEFAULT_SEED = 20250221
+
+
+def _torch():
+    import torch
+    return torch
+
+
+@dataclass
+class BatchResult:
+    fail: np.ndarray          # bool[B]
+    bp_converged: int
+    iters_sum: int
+    ssf_steps_sum: int
+    corrections: np.ndarray | None = None  # uint8[B, n] when requested
+
+
+class BatchPipeline:
+    """One decoder mode on one device.  ``run(syn, readout)`` takes the sampler's
+    device tensors (spacetime syndrome uint8[B,(R+1)m], readout uint8[B,n])."""
+
+    def __init__(self, code, rounds: int, mode: str, bp_osd_options: Dict, priors: Tuple[float, float], *,
+                 device: int = 0, precision: str = "f32", use_x_logicals: bool = False, osd_threads: int = 0):
+        if mode == "bpd_detector":
+            raise NotImplementedError("decoder_mode 'bpd_detector' needs a Stim detector error model "
+                                      "(DetectorSpacetimeCode); not supported by this build")
+        if mode not in DECODER_MODES:
+            raise RuntimeError("Unknown decoder operation mode")
+        if mode == "bpssf" and rounds > 0:
+            mode = "bpssf_hybrid"
+        self.mode = mode
+        self.R = int(rounds)
+        self.device = int(device)
+        data_prior, meas_prior = priors
+        H = code.checks.x if use_x_logicals else code.checks.z
+        G = code.checks.z if use_x_logicals else code.checks.x
+        L = code.logicals.x if use_x_logicals else code.logicals.z
+        self.H = sp.csr_matrix(H)
+        self.m, self.n = self.H.shape
+        self.L = np.asarray(L) % 2
+        o = bp_osd_options
+        common = dict(method=o.get("bp_method", "ps"), precision=precision, max_iter=int(o.get("max_iter", 0) or 0),
+                      ms_scaling=float(o.get("ms_scaling_factor", 0.0)), device=self.device)
+        osd_method = o.get("osd_method", "osd_cs")
+        osd_order = int(o.get("osd_order", 0))
+        self.osd_threads = osd_threads
+        R, n = self.R, self.n
+        lz = self.L if self.L.shape[0] else None
+        # spacetime stage (modes that use it)
+        if mode in ("bposd", "bposd_hybrid", "bpssf_hybrid", "bp"):
+            st = SpacetimeCode(self.H, R)
+            Hst = st.spacetime_check_matrix
+            prior = np.empty(Hst.shape[1])
+            prior[st.true_data_slice()] = data_prior
+            prior[(R + 1) * n:] = meas_prior
+            self.st = Decoder(Hst, prior, n_data=n, fold_blocks=R + 1, logicals=lz, **common)
+            self.st_osd = OsdSolver(Hst, osd_method, osd_order, osd_threads) if mode == "bposd" else None
+        # final-round stage on H
+        if mode in ("bposd_hybrid", "bposd_single_shot"):
+            self.fin = Decoder(self.H, data_prior, logicals=lz, **common)
+            self.fin_osd = OsdSolver(self.H, osd_method, osd_order, osd_threads)
+        if mode in ("bpssf", "bpssf_hybrid"):
+            self.fin = Decoder(self.H, data_prior, logicals=lz, flip_sets=G, ssf=True, **common)
+        if mode == "bposd_single_shot":
+            ss = SpacetimeCodeSingleShot(self.H)
+            Hss = ss.spacetime_check_matrix
+            prior = np.empty(Hss.shape[1])
+            prior[:n] = data_prior
+            prior[n:] = meas_prior
+            self.ss = Decoder(Hss, prior, n_data=n, fold_blocks=1, **common)
+            self.ss_osd = OsdSolver(Hss, osd_method, osd_order, osd_threads)
+        # a plain-H decoder for the sampler
+        self.sampler_graph = Decoder(self.H, 0.01, device=self.device)
+
+    # ----------------------------------------------------------- helpers
+    def _fail_host(self, readout, corr):
+        if self.L.shape[0] == 0:
+            return np.zeros(readout.shape[0], bool)
+        return ((((readout ^ corr).astype(np.int64)) @ self.L.T.astype(np.int64)) % 2).any(axis=1)
+
+    def _osd_fix(self, dec, osd, syn_d, status_d, llr_d, B):
+        """OSD for shots whose BP did not converge; returns (idx, osdw) on host."""
+        torch = _torch()
+        bad = torch.nonzero((status_d & 1) == 0).flatten()
+        if bad.numel() == 0:
+            return None, None
+        idx = bad.cpu().numpy()
+        s = syn_d.index_select(0, bad).cpu().numpy()
+        llr = llr_d.index_select(0, bad).double().cpu().numpy()
+        _, ow = osd.solve(s, llr)
+        return idx, ow
+
+    def run(self, syn, readout, want_corrections: bool = False) -> BatchResult:
+        torch = _torch()
+        B = syn.shape[0]
+        dev = syn.device
+        u8 = dict(dtype=torch.uint8, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        n, m, R = self.n, self.m, self.R
+        iters = torch.zeros(B, **i32)
+        status = torch.zeros(B, **u8)
+        fail = torch.zeros(B, **u8)
+        steps = torch.zeros(B, **i32)
+        corr = torch.zeros((B, n), **u8)
+        host_fix = None  # (idx, corrections) applied on host
+        mode = self.mode
+        if mode in ("bp", "bposd"):
+            need_llr = mode == "bposd"
+            llr = torch.empty((B, self.st.n), dtype=torch.float32 if self.st.precision == _abi.QD_F32
+                              else torch.float64, device=dev) if need_llr else None
+            self.st.decode_device(B, syn=syn, readout=readout, corr=corr, llr=llr, iters=iters, status=status,
+                                  fail=fail)
+            if need_llr:
+                idx, ow = self._osd_fix(self.st, self.st_osd, syn, status, llr, B)
+                if idx is not None:
+                    fold = np.zeros((idx.size, n), np.uint8)
+                    for t in range(R + 1):
+                        fold ^= ow[:, t * n:(t + 1) * n]
+                    host_fix = (idx, fold)
+        elif mode in ("bposd_hybrid", "bpssf_hybrid"):
+            c1 = torch.empty((B, n), **u8)
+            self.st.decode_device(B, syn=syn, corr=c1, iters=iters)
+            if mode == "bpssf_hybrid":
+                self.fin.decode_device(B, base=c1, readout=readout, corr=corr, status=status, ssf_steps=steps,
+                                       fail=fail, syn_flags=3)
+            else:
+                llr = torch.empty((B, n), dtype=torch.float32 if self.fin.precision == _abi.QD_F32
+                                  else torch.float64, device=dev)
+                self.fin.decode_device(B, base=c1, readout=readout, corr=corr, llr=llr, status=status, fail=fail,
+                                       syn_flags=3)
+                bad = torch.nonzero((status & 1) == 0).flatten()
+                if bad.numel():
+                    idx = bad.cpu().numpy()
+                    v = (readout.index_select(0, bad) ^ c1.index_select(0, bad)).cpu().numpy()
+                    s2 = ((self.H @ v.T).T % 2).astype(np.uint8)
+                    _, ow = self.fin_osd.solve(s2, llr.index_select(0, bad).double().cpu().numpy())
+                    host_fix = (idx, c1.index_select(0, bad).cpu().numpy() ^ ow)
+        elif mode == "bpssf":
+            self.fin.decode_device(B, syn=syn, readout=readout, corr=corr, iters=iters, status=status,
+                                   ssf_steps=steps, fail=fail)
+        elif mode == "bposd_single_shot":
+            acc = torch.zeros((B, n), **u8)
+            raw = torch.zeros((B, m), **u8)
+            sv = syn.view(B, R + 1, m)
+            Hss_n = self.ss.n
+            for t in range(R):
+                raw ^= sv[:, t]
+                st_t = torch.zeros(B, **u8)
+                llr = torch.empty((B, Hss_n), dtype=torch.float32 if self.ss.precision == _abi.QD_F32
+                                  else torch.float64, device=dev)
+                new_acc = torch.empty((B, n), **u8)
+                s_in = raw.contiguous()
+                self.ss.decode_device(B, syn=s_in, base=acc, corr=new_acc, llr=llr, status=st_t, syn_flags=1)
+                bad = torch.nonzero((st_t & 1) == 0).flatten()
+                if bad.numel():
+                    a_h = acc.index_select(0, bad).cpu().numpy()
+                    s_h = s_in.index_select(0, bad).cpu().numpy() ^ ((self.H @ a_h.T).T % 2).astype(np.uint8)
+                    _, ow = self.ss_osd.solve(s_h, llr.index_select(0, bad).double().cpu().numpy())
+                    new_acc[bad] = torch.from_numpy(a_h ^ ow[:, :n]).to(dev)
+                acc = new_acc
+            llr = torch.empty((B, n), dtype=torch.float32 if self.fin.precision == _abi.QD_F32 else torch.float64,
+                              device=dev)
+            self.fin.decode_device(B, base=acc, readout=readout, corr=corr, llr=llr, iters=iters, status=status,
+                                   fail=fail, syn_flags=3)
+            bad = torch.nonzero((status & 1) == 0).flatten()
+            if bad.numel():
+                idx = bad.cpu().numpy()
+                a_h = acc.index_select(0, bad).cpu().numpy()
+                v = readout.index_select(0, bad).cpu().numpy() ^ a_h
+                s2 = ((self.H @ v.T).T % 2).astype(np.uint8)
+                _, ow = self.fin_osd.solve(s2, llr.index_select(0, bad).double().cpu().numpy())
+                host_fix = (idx, a_h ^ ow)
+        fail_h = fail.cpu().numpy().astype(bool)
+        corr_h = corr.cpu().numpy() if (want_corrections or host_fix is not None) else None
+        if host_fix is not None:
+            idx, c = host_fix
+            corr_h[idx] = c
+            fail_h[idx] = self._fail_host(readout.index_select(0, torch.from_numpy(idx).to(dev)).cpu().numpy(), c)
+        return BatchResult(fail=fail_h, bp_converged=int((status & 1).sum().item()),
+                           iters_sum=int(iters.to(torch.int64).sum().item()),
+                           ssf_steps_sum=int(steps.to(torch.int64).sum().item()),
+                           corrections=corr_h if want_corrections else None)
+
+
+# ------------------------------------------------------------------ per-shot API
+class _PerShot:
+    """Reference-style wrapper: ``readout_correction(history, readout)`` for one
+    shot (history(t) = Z-check outcomes of round t), via a batch of 1."""
+
+    mode = "bposd"
+
+    def __init__(self, code, rounds: int, bp_osd_options: Dict, priors: Tuple[float, float], **kw):
+        self._code = code
+        self._rounds = int(rounds)
+        self._pipe = BatchPipeline(code, rounds, self.mode, bp_osd_options, priors, **kw)
+
+    def readout_correction(self, history: Callable[[int], np.ndarray], readout) -> np.ndarray:
+        torch = _torch()
+        H = self._pipe.H
+        R = self._rounds
+        readout = np.asarray(readout, dtype=np.uint8) % 2
+        rows = [np.asarray(history(t), dtype=np.uint8) % 2 for t in range(R)]
+        from .spacetime import spacetime_syndrome_batch
+        hist = np.stack(rows)[None] if R else np.zeros((1, 0, H.shape[0]), np.uint8)
+        syn = spacetime_syndrome_batch(R, H, hist, readout[None])
+        dev = torch.device("cuda", self._pipe.device)
+        res = self._pipe.run(torch.from_numpy(syn).to(dev), torch.from_numpy(readout[None].copy()).to(dev),
+                             want_corrections=True)
+        return res.corrections[0].astype(np.int64)
+
+
+class BPOSDCorrect(_PerShot):
+    mode = "bposd"
+
+
+class BPOSDHybridCorrect(_PerShot):
+    mode = "bposd_hybrid"
+
+
+class BPOSDCorrectSingleShot(_PerShot):
+    mode = "bposd_single_shot"
+
+
+class BPSSFCorrect(_PerShot):
+    mode = "bpssf"
+
+
+class BPSSFHybridCorrect(_PerShot):
+    mode = "bpssf_hybrid"
+
+
+# ------------------------------------------------------------------ simulation
+def _steps(checks):
+    def mx(a):
+        a = sp.csr_matrix(a)
+        return max(int(a.sum(axis=0).max()), int(a.sum(axis=1).max()))
+    return mx(checks.x), mx(checks.z)
+
+
+def run_simulation(samples, code, meas_prior, data_prior, noise_model, noise_model_args, bp_osd_options, rounds,
+                   decoder_mode, *, seed: int = DEFAULT_SEED, stream_id: int = 0, shot0: int = 0, device: int = 0,
+                   batch: int = 1 << 18, precision: str = "f32", stats: dict | None = None):
+    """Sample and decode `samples` shots on one GPU; returns a bool ndarray of
+    logical-failure flags (reference run_simulation, _experiment.py:154-210,
+    which returns a list of the same flags)."""
+    torch = _torch()
+    x_steps, z_steps = _steps(code.checks)
+    sim = build_storage_simulation(rounds, noise_model(**noise_model_args), code, use_x_logicals=False)
+    mp = meas_prior(x_steps, z_steps)
+    dp = data_prior(x_steps, z_steps)
+    pipe = BatchPipeline(code, rounds, decoder_mode, bp_osd_options, (dp, mp), device=device, precision=precision)
+    out = np.zeros(samples, dtype=bool)
+    agg = {"bp_converged": 0, "iters_sum": 0, "ssf_steps_sum": 0}
+    with torch.cuda.device(device):
+        for start in range(0, samples, batch):
+            b = min(batch, samples - start)
+            syn, rd = sim.sample_device(pipe.sampler_graph, b, seed, stream_id, shot0 + start)
+            res = pipe.run(syn, rd)
+            out[start:start + b] = res.fail
+            agg["bp_converged"] += res.bp_converged
+            agg["iters_sum"] += res.iters_sum
+            agg["ssf_steps_sum"] += res.ssf_steps_sum
+    if stats is not None:
+        stats.update(agg)
+    return out
+
+
+def add_bposd_args(parser):
+    """BP+OSD options (reference add_bposd_args, _experiment.py:213-219)."""
+    parser.add_argument("--bposd_max_iter", type=lambda x: int(x) if x is not None else None,
+                        help="Maximum number of iterations for BP. Default is the number of qubits in the code",
+                        default=None)
+    parser.add_argument("--bposd_bp_method", choices=["ps", "ms", "msl"],
+                        help="BP method (product-sum, min-sum, min-sum log)", default="ps")
+    parser.add_argument("--bposd_ms_scaling_factor", type=float,
+                        help="Min sum scaling factor. Use variable scaling factor method if 0", default=0)
+    parser.add_argument("--bposd_osd_method", choices=["osd_e", "osd_cs", "osd0"], help="OSD method", default="osd_cs")
+    parser.add_argument("--bposd_osd_order", type=int, help="OSD search depth", default=7)
+
+
+def unpack_bposd_args(parsed_args, code):
+    """Reference unpack_bposd_args (_experiment.py:221-229): max_iter defaults to
+    the number of qubits."""
+    return {
+        "max_iter": parsed_args.bposd_max_iter if parsed_args.bposd_max_iter is not None else code.checks.num_qubits,
+        "bp_method": parsed_args.bposd_bp_method,
+        "ms_scaling_factor": parsed_args.bposd_ms_scaling_factor,
+        "osd_method": parsed_args.bposd_osd_method,
+        "osd_order": parsed_args.bposd_osd_order,
+    }
+
+
+def load_code(args):
+    with Path(args.code).open() as f:
+        return read_quantum_code(f, validate_stabilizer_code=True)
+
+
+# ------------------------------------------------------------------ sweep
+def _device_count() -> int:
+    try:
+        return max(1, _abi.load().qd_device_count())
+    except Exception:
+        return 1
+
+
+def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_prior, *, gpus: int | None = None,
+            seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f32", **kwargs):
+    """Sweep the physical error rate (reference p_sweep, misc/p_sweep.py:17-40).
+    Shots are sharded over `gpus` devices by index (device d decodes a
+    contiguous shot range); exactly `samples` shots per point."""
+    import pandas as pd
+    torch = _torch()
+    ndev = gpus or _device_count()
+    code = kwargs["code"]
+    rounds = kwargs["rounds"]
+    mode = kwargs["decoder_mode"]
+    bp_osd_options = kwargs["bp_osd_options"]
+    x_steps, z_steps = _steps(code.checks)
+    data = []
+    for pi, p_ph in enumerate(p_values):
+        t0 = time.perf_counter()
+        nm = noise_model(**noise_model_args(p_ph))
+        sim = build_storage_simulation(rounds, nm, code, use_x_logicals=False)
+        dp = data_prior(p_ph, x_steps, z_steps)
+        mp = meas_prior(p_ph, x_steps, z_steps)
+        pipes = [BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision)
+                 for d in range(ndev)]
+        per = math.ceil(samples / ndev)
+        failures = conv = iters = ssf = 0
+        for d, pipe in enumerate(pipes):
+            lo, hi = d * per, min(samples, (d + 1) * per)
+            with torch.cuda.device(d):
+                for start in range(lo, hi, batch):
+                    b = min(batch, hi - start)
+                    syn, rd = sim.sample_device(pipe.sampler_graph, b, seed, pi, start)
+                    res = pipe.run(syn, rd)
+                    failures += int(res.fail.sum())
+                    conv += res.bp_converged
+                    iters += res.iters_sum
+                    ssf += res.ssf_steps_sum
+        for d in range(ndev):
+            torch.cuda.synchronize(d)
+        runtime = time.perf_counter() - t0
+        point = {"p_ph": p_ph, "failures": failures, "samples": samples, "walltime": runtime, **kwargs,
+                 **bp_osd_options, "gpus": ndev, "shots_per_s": samples / runtime if runtime > 0 else float("nan"),
+                 "bp_converged_frac": conv / samples if samples else 0.0,
+                 "iters_mean": iters / samples if samples else 0.0,
+                 "ssf_steps_mean": ssf / samples if samples else 0.0}
+        del point["code"]
+        del point["bp_osd_options"]
+        data.append(point)
+    return pd.DataFrame.from_records(data)
+
+
+_SWEEP_RE = re.compile(r"^\s*[(](.+),(.+),(.+)[)]\s*$")
+
+
+def parse_sweep_spec(x: str) -> Tuple[float, float, int]:
+    """'(a, b, c)' -> (float, float, int), a <= b, c > 0 (misc/p_sweep.py:43-55)."""
+    r = _SWEEP_RE.match(x)
+    if r is None:
+        raise RuntimeError("Unable to parse sweep specification, expecting (a, b, c) where a,b : float, c : int, "
+                           "a<=b, and c > 0. Ex: (0.3, 1e3, 10)")
+    lo, hi, pts = float(r.group(1)), float(r.group(2)), int(r.group(3))
+    if pts <= 0 or lo > hi:
+        raise RuntimeError("Number of points non-positive or lower bound exceeded upper bound")
+    return lo, hi, pts
+
+
+def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
+    """CLI of the sweep (reference p_sweep_main, misc/p_sweep.py:57-78); extra
+    flags: --gpus, --seed, --batch, --precision; extra decoder modes bpssf,
+    bpssf_hybrid, bp."""
+    parser = ArgumentParser(description="Perform a parallelized sweep in the physical error rate for the given "
+                                        "quantum code under BP+OSD / BP+SSF on MI355X")
+    parser.add_argument("code", type=Path)
+    parser.add_argument("--samples", type=int, help="Number of samples to take")
+    parser.add_argument("--p_sweep", type=parse_sweep_spec,
+                        help="Specify lower and upper bounds of the sweep + number of points in the form "
+                             "(lower, upper, points)")
+    parser.add_argument("--rounds", type=int, help="Number of rounds of syndrome extraction", default=1)
+    parser.add_argument("--decoder_mode", choices=DECODER_MODES, default="bposd",
+                        help="Operate decoder in BP+OSD, BP+OSD (single shot), hybrid BP + (BP+OSD), or BP+SSF")
+    parser.add_argument("--linspace", type=bool, default=False,
+                        help="Perform the sweep with linearly spaced points. The default is uniform spacing in log "
+                             "space")
+    add_bposd_args(parser)
+    parser.add_argument("--gpus", type=int, default=None, help="GPUs to shard shots over (default: all visible)")
+    parser.add_argument("--seed", type=int, default=DEFAULT_SEED, help="sampler seed (counter-based Philox)")
+    parser.add_argument("--batch", type=int, default=1 << 18, help="shots per device launch")
+    parser.add_argument("--precision", choices=["f32", "f64"], default="f32", help="BP message precision")
+    args = parser.parse_args(sys.argv[1:])
+    code = load_code(args)
+    bp_osd_options = unpack_bposd_args(args, code)
+    sweep = np.linspace(*args.p_sweep) if args.linspace else np.geomspace(*args.p_sweep)
+    result = p_sweep(samples=args.samples, code=code, rounds=args.rounds, noise_model=noise_model,
+                     noise_model_args=noise_model_args, meas_prior=meas_prior, data_prior=data_prior,
+                     p_values=sweep, decoder_mode=args.decoder_mode, bp_osd_options=bp_osd_options,
+                     gpus=args.gpus, seed=args.seed, batch=args.batch, precision=args.precision)
+    result.to_csv(sys.stdout)
+    return result

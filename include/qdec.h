@@ -121,6 +121,17 @@ int qd_sample_storage_device(qd_graph* g, int32_t rounds, double p_data, double 
                              uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
                              uint8_t* syn, uint8_t* readout, void* stream);
 
+/* Ordered-statistics decoding of shots BP did not converge on (the OSD stage of
+ * ldpc v1 bposd_decoder; reference _experiment.py:23-27, 37-40, 77, 96-100).  Host
+ * buffers; runs on the host cores (nthreads <= 0: all).  method: 0 = osd0,
+ * 1 = osd_e, 2 = osd_cs; order = osd_order.  llr = BP log-probability ratios
+ * (qd_decode_batch llr_out widened to double).  Outputs osd0 and the best
+ * higher-order solution (ldpc .osd0_decoding / .osdw_decoding), uint8 [B][n]. */
+int qd_osd_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx, int32_t method,
+                 int32_t order, int64_t B, const uint8_t* syn, const double* llr, uint8_t* osd0_out,
+                 uint8_t* osdw_out, int32_t nthreads);
+const char* qd_osd_last_error(void);
+
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */
 int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream);

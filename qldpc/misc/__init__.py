@@ -1,0 +1,2 @@
+"""qldpc.misc compatibility module (reference python/qldpc/misc/__init__.py)."""
+from exp_ldpc_amd.experiment import p_sweep, p_sweep_main, run_simulation  # noqa: F401

@@ -1,0 +1,134 @@
+"""CPU-side checks of the product library and host logic: the C ABI loads and
+exports every symbol include/qdec.h declares, constructors fail loudly without
+a GPU, OSD (host C++ in libqdec_hip.so) matches its independent checker, and the
+harness argument handling mirrors the reference."""
+import argparse
+
+import numpy as np
+import pytest
+
+from conftest import load_checks
+
+HX, HZ = load_checks("hgp_12_3_4_s1234")
+
+
+def test_library_exports_every_header_symbol():
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    syms = _abi.header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _abi.SIGNATURES, f"{s} has no ctypes signature"
+    assert lib.qd_abi_version() == 1
+
+
+def test_no_cpu_fallback_without_gpu():
+    """On a machine without a HIP device the decoder refuses to construct."""
+    from exp_ldpc_amd import _abi
+    from exp_ldpc_amd.decoder import Decoder
+    if _abi.load().qd_device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(_abi.QdecError):
+        Decoder(HZ, 0.01)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from exp_ldpc_amd import _abi
+    with pytest.raises(_abi.QdecError):
+        _abi.load(str(tmp_path / "nope.so"))
+
+
+@pytest.mark.parametrize("method,order", [("osd0", 0), ("osd_cs", 7), ("osd_cs", 3), ("osd_e", 4)])
+def test_osd_matches_checker(method, order):
+    from exp_ldpc_amd.osd import OsdSolver
+    from oracle.osd_py import osd_decode
+    rng = np.random.default_rng(order)
+    B = 20
+    e = (rng.random((B, 225)) < 0.05).astype(np.uint8)
+    syn = ((HZ @ e.T).T % 2).astype(np.uint8)
+    llr = rng.normal(3, 3, (B, 225))
+    llr[:, :10] = 1.0  # ties: order by column index
+    o0, ow = OsdSolver(HZ, method, order).solve(syn, llr)
+    for b in range(B):
+        r0, rw = osd_decode(HZ, syn[b], llr[b], method, order)
+        assert np.array_equal(o0[b], r0) and np.array_equal(ow[b], rw)
+        assert ((HZ @ ow[b]) % 2 == syn[b]).all()
+        assert ow[b].sum() <= o0[b].sum()
+
+
+def test_osd_on_spacetime_matrix():
+    from exp_ldpc_amd.osd import OsdSolver
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    from oracle.osd_py import osd_decode
+    H = SpacetimeCode(HZ, 1).spacetime_check_matrix
+    rng = np.random.default_rng(9)
+    e = (rng.random((6, H.shape[1])) < 0.03).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    llr = rng.normal(2, 2, (6, H.shape[1]))
+    o0, ow = OsdSolver(H, "osd_cs", 7).solve(syn, llr)
+    for b in range(6):
+        r0, rw = osd_decode(H, syn[b], llr[b], "osd_cs", 7)
+        assert np.array_equal(ow[b], rw)
+
+
+def test_bp_method_names():
+    from exp_ldpc_amd import _abi
+    from exp_ldpc_amd.decoder import parse_bp_method
+    for name in ("ps", "product_sum", 0, "0"):
+        assert parse_bp_method(name) == _abi.QD_PRODUCT_SUM
+    for name in ("ms", "msl", "minimum_sum", "minimum_sum_log", "min_sum", 1, 3):
+        assert parse_bp_method(name) == _abi.QD_MIN_SUM
+    with pytest.raises(NotImplementedError):
+        parse_bp_method("ps_log")
+    with pytest.raises(ValueError):
+        parse_bp_method("bogus")
+
+
+def test_ldpc_kwargs_resolution():
+    from exp_ldpc_amd.ldpc_compat import _resolve_probs
+    assert np.allclose(_resolve_probs(4, {"error_rate": 0.1}), 0.1)
+    assert np.allclose(_resolve_probs(3, {"channel_probs": [0.1, 0.2, 0.3]}), [0.1, 0.2, 0.3])
+    assert np.allclose(_resolve_probs(2, {"channel_prior": [0.1, 0.2]}), [0.1, 0.2])  # _experiment.py:77
+    assert np.allclose(_resolve_probs(2, {"channel_probs": [None], "error_rate": 0.3}), 0.3)
+    with pytest.raises(ValueError):
+        _resolve_probs(3, {})
+    with pytest.raises(ValueError):
+        _resolve_probs(3, {"channel_probs": [0.1, 0.2]})
+
+
+def test_harness_arguments_mirror_reference():
+    from exp_ldpc_amd.codes import QuantumCode, QuantumCodeChecks
+    from exp_ldpc_amd.experiment import add_bposd_args, parse_sweep_spec, unpack_bposd_args
+    p = argparse.ArgumentParser()
+    add_bposd_args(p)
+    a = p.parse_args([])
+    code = QuantumCode(QuantumCodeChecks(HX, HZ))
+    opts = unpack_bposd_args(a, code)
+    assert opts == {"max_iter": 225, "bp_method": "ps", "ms_scaling_factor": 0, "osd_method": "osd_cs",
+                    "osd_order": 7}
+    assert parse_sweep_spec("(1e-3, 1e-1, 9)") == (1e-3, 1e-1, 9)
+    with pytest.raises(RuntimeError):
+        parse_sweep_spec("(0.2, 0.1, 3)")
+    with pytest.raises(RuntimeError):
+        parse_sweep_spec("0.1,0.2")
+
+
+def test_qldpc_shim_surface():
+    import qldpc
+    import qldpc.misc
+    assert callable(qldpc.misc.p_sweep_main)
+    nm = qldpc.noise_model.depolarizing_noise(0.01, 0.01)
+    assert nm.kind == "depolarizing"
+    assert qldpc.read_quantum_code is not None and qldpc.SpacetimeCode is not None
+
+
+def test_sharding_arithmetic():
+    from exp_ldpc_amd.sharding import shard_range, step_shot0
+    assert [shard_range(10, 3, r) for r in range(3)] == [(0, 4), (4, 8), (8, 10)]
+    seen = set()
+    for s in range(3):
+        for r in range(4):
+            lo = step_shot0(s, 4, r, 5)
+            seen.update(range(lo, lo + 5))
+    assert seen == set(range(60))

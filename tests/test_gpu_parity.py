@@ -192,3 +192,68 @@ def test_random_irregular_codes(gpu_available, oracle_lib, seed):
             for key in ("x", "iters", "status"):
                 assert np.array_equal(got[key], ref[key]), (method, precision, key)
             _cmp_llr(got["llr"], ref["llr"], method, precision)
+
+
+def _graph(name):
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    if name.startswith("st"):  # st<R>_<code>
+        R, code = name[2], name[4:]
+        return SpacetimeCode(load_checks(code)[1], int(R)).spacetime_check_matrix, None
+    hx, hz = load_checks(name)
+    return hz, hx
+
+
+BLOCK_GRAPHS = ["hgp_24_3_4_s11", "hgp_36_3_4_s42_g4", "st2_hgp_12_3_4_s1234", "st3_hgp_12_3_4_s1234",
+                "st1_hgp_36_3_4_s42_g4"]
+
+
+@pytest.mark.parametrize("name", BLOCK_GRAPHS)
+@pytest.mark.parametrize("method,precision", [("ms", "f32"), ("ps", "f64"), ("ms", "f64")])
+def test_block_kernel_parity(gpu_available, oracle_lib, name, method, precision):
+    """Graphs outside the wave shapes (n > 576, row degree 9 at R >= 2, HBM
+    message scratch for the 36x36 spacetime graph) take the workgroup kernels."""
+    from exp_ldpc_amd.decoder import Decoder
+    H, _ = _graph(name)
+    H = sp.csr_matrix(H)
+    rng = np.random.default_rng(len(name))
+    B = 300
+    e = (rng.random((B, H.shape[1])) < 0.02).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    dec = Decoder(H, 0.015, method=method, precision=precision, max_iter=25)
+    got = dec.decode(syn, want=("x", "llr", "iters", "status"))
+    ref = oracle_lib.decode(H, 0.015, syn, method=method, precision=precision, max_iter=25)
+    for key in ("x", "iters", "status"):
+        assert np.array_equal(got[key], ref[key]), key
+    _cmp_llr(got["llr"], ref["llr"], method, precision)
+
+
+@pytest.mark.parametrize("name", ["hgp_24_3_4_s11", "hgp_36_3_4_s42_g4"])
+def test_block_ssf_parity(gpu_available, oracle_lib, name):
+    from conftest import load_code
+    from exp_ldpc_amd.decoder import Decoder
+    code = load_code(name)
+    hx, hz = code.checks.x, code.checks.z
+    rng = np.random.default_rng(5)
+    B = 400
+    rd = (rng.random((B, hz.shape[1])) < 0.03).astype(np.uint8)
+    syn = ((hz @ rd.T).T % 2).astype(np.uint8)
+    dec = Decoder(hz, 0.02, method="ms", precision="f32", max_iter=8, flip_sets=hx, logicals=code.logicals.z)
+    got = dec.decode(syn, readout=rd, want=("x", "corr", "iters", "status", "ssf_steps", "fail"))
+    ref = oracle_lib.decode(hz, 0.02, syn, method="ms", precision="f32", max_iter=8, ssf=True, gens=hx,
+                            lz=code.logicals.z, readout=rd, want_llr=False, ssf_impl="fast")
+    for key in ("x", "corr", "iters", "status", "ssf_steps", "fail"):
+        assert np.array_equal(got[key], ref[key]), key
+    assert ref["ssf_steps"].sum() > 0
+
+
+def test_spacetime_r2_fold(gpu_available, oracle_lib, code225):
+    from exp_ldpc_amd.decoder import Decoder
+    H = _spacetime(2)
+    syn, rd = oracle_lib.sample_storage(HZ, 2, 0.01, 0.01, seed=8, stream=0, shot0=0, B=800)
+    lz = code225.logicals.z
+    dec = Decoder(H, 0.0067, method="ms", precision="f32", max_iter=30, n_data=225, fold_blocks=3, logicals=lz)
+    got = dec.decode(syn, readout=rd, want=("corr", "iters", "status", "fail"))
+    ref = oracle_lib.decode(H, 0.0067, syn, method="ms", precision="f32", max_iter=30, n_data=225, fold_blocks=3,
+                            lz=lz, readout=rd, want_llr=False)
+    for key in ("corr", "iters", "status", "fail"):
+        assert np.array_equal(got[key], ref[key]), key
