@@ -13,9 +13,10 @@ shots are sharded by index (rank r decodes shot range r*B..), no data-path
 collective; a barrier + synchronize brackets the timed region and rank 0 reports
 the max time over ranks.  value = shots decoded by all ranks / that time.
 
-Also reported: `roofline` for the decode kernel (algorithmic bytes per launch per
-SURVEY §8(d): 334 B/shot of I/O + 16*E B per BP iteration, over the average
-launch duration measured with HIP events on the launch stream), and
+Also reported: `roofline` for the BP kernel (algorithmic bytes per launch per
+SURVEY §8(d): 334 B/shot of I/O + 16*E B per BP iteration, over the BP kernel's
+average launch duration measured with HIP events the library records on the
+launch stream immediately around it; the SSF kernel's time is listed beside), and
 `cpu_baseline`: the CPU oracle (oracle/, a C port of the same algorithm, OpenMP)
 timed on the host cores on a bounded sample of the same workload (rank 0, N=1).
 """
@@ -102,7 +103,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 18, help="shots per sweep point per step per GPU")
     ap.add_argument("--points", type=int, default=9)
     ap.add_argument("--p", type=float, action="append", help="decode only these p values (diagnostics)")
-    ap.add_argument("--cpu-shots", type=int, default=20000, help="CPU-baseline shots per sweep point")
+    ap.add_argument("--cpu-shots", type=int, default=200000, help="CPU-baseline shots per sweep point")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -148,20 +149,19 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in ps]
-          for _ in range(nsteps)]
 
     def step(s):
         for pi in range(len(ps)):
-            e0, e1 = ev[s][pi]
-            e0.record(stream)
             decs[pi].decode_device(B, syn=syn[s, pi], readout=rd[s, pi], iters=iters[s, pi], status=status[s, pi],
                                    fail=fail[s, pi], stream=stream.cuda_stream)
-            e1.record(stream)
 
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
+    # HIP events recorded by the library on the launch stream right before the
+    # BP kernel, after it and after the SSF kernel of every timed call
+    for d in decs:
+        d.set_timing(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -179,8 +179,13 @@ def main():
         elapsed = float(tt.item())
 
     # ---- per-launch kernel times and algorithmic bytes ----
-    timed = range(args.warmup, nsteps)
-    launch_ms = np.array([[ev[s][pi][0].elapsed_time(ev[s][pi][1]) for pi in range(len(ps))] for s in timed])
+    bp_ms = np.zeros((args.steps, len(ps)))
+    ssf_ms = np.zeros((args.steps, len(ps)))
+    for pi, d in enumerate(decs):
+        a, c = d.read_timing()
+        bp_ms[:, pi] = a
+        ssf_ms[:, pi] = c
+    launch_ms = bp_ms
     it_sum = iters[args.warmup:].to(torch.int64).sum(dim=2).cpu().numpy()  # [steps, points]
     b_io = m + n + 1  # syndrome in + correction out + failure flag
     bytes_per_launch = b_io * B + 16 * E * it_sum  # [steps, points]
@@ -206,7 +211,8 @@ def main():
                                "ler": float(fails[pi] / shots_per_point), "wilson95": [lo, hi],
                                "bp_converged_frac": float(conv[pi] / shots_per_point),
                                "mean_bp_iters_rank0": float(itp[pi]),
-                               "kernel_ms_per_launch": float(launch_ms[:, pi].mean())}
+                               "bp_kernel_ms_per_launch": float(bp_ms[:, pi].mean()),
+                               "ssf_kernel_ms_per_launch": float(ssf_ms[:, pi].mean())}
         traffic = latest_traffic()
         result = {
             "metric": METRIC, "value": value, "unit": "shots/s", "n_gpus": world, "steps": args.steps,
@@ -221,8 +227,11 @@ def main():
                        "parallelism": f"shot-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "bp_wave_kernel<float,MS,2,4>",
+                         "kernel": "bp_wave_kernel<float, 1, 2, 4, 7, true> (BP min-sum, fp32, queues BP failures)",
                          "avg_launch_ms": float(launch_ms.mean()),
+                         "launches": int(launch_ms.size),
+                         "ssf_kernel": "ssf_wave_kernel<2>", "ssf_avg_launch_ms": float(ssf_ms.mean()),
+                         "timing": "HIP events recorded by the library on the launch stream around each kernel",
                          "algorithmic_bytes_per_launch": float(bytes_per_launch.mean()),
                          "bytes_model": "per shot: (m+n+1)=334 B I/O + 16*E=12096 B per BP iteration"},
             "ler": ler,

@@ -87,6 +87,9 @@ struct qd_graph {
     // HBM message scratch for the workgroup kernels on graphs too large for LDS
     void* mws = nullptr;
     size_t mws_bytes = 0;
+    // kernel timing ring (qd_graph_set_timing): 3 events per decode call
+    std::vector<hipEvent_t> tev;
+    int t_cap = 0, t_count = 0;
 };
 
 namespace {
@@ -228,6 +231,17 @@ void* message_scratch(qd_graph* G, int precision, size_t* bytes) {
     return G->mws;
 }
 
+void attach_timing(qd_graph* G, DecodeArgs& a) {
+    a.ev = nullptr;
+    if (G->t_cap > 0 && G->t_count < G->t_cap) a.ev = &G->tev[(size_t)3 * G->t_count++];
+}
+
+void free_timing(qd_graph* G) {
+    for (hipEvent_t e : G->tev) (void)hipEventDestroy(e);
+    G->tev.clear();
+    G->t_cap = G->t_count = 0;
+}
+
 void check_graph(const qd_graph* g) {
     if (!g) throw Fail(-1, "null graph handle");
 }
@@ -337,6 +351,7 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->ws) (void)hipFree(g->ws);
         if (g->qws) (void)hipFree(g->qws);
         if (g->mws) (void)hipFree(g->mws);
+        free_timing(g);
         if (g->stream) (void)hipStreamDestroy(g->stream);
         delete g;
     });
@@ -462,6 +477,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         set_device(G);
         DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
         attach_queue(G, a);
+        attach_timing(G, a);
         size_t sb = 0;
         void* scr = message_scratch(G, p->precision, &sb);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream, scr, sb);
@@ -515,6 +531,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
                                  (const uint8_t*)dptr(r_rd), (uint8_t*)dptr(r_x), (uint8_t*)dptr(r_corr), dptr(r_llr),
                                  (int32_t*)dptr(r_it), (uint8_t*)dptr(r_st), (int32_t*)dptr(r_ss), (uint8_t*)dptr(r_fl));
         attach_queue(G, a);
+        attach_timing(G, a);
         size_t sb = 0;
         void* scr = message_scratch(G, p->precision, &sb);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
@@ -549,6 +566,39 @@ int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double 
         const int rc = launch_sample_storage(G->dg, rounds, thr(2.0 * p_data / 3.0), thr(p_meas), seed, stream_id,
                                              shot0, B, syn, readout, G->num_cus, (hipStream_t)stream);
         if (rc != 0) throw Fail(-102, std::string("sampler launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
+int qd_graph_set_timing(qd_graph* G, int32_t capacity) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        if (capacity < 0) throw Fail(-90, "negative timing capacity");
+        free_timing(G);
+        G->tev.resize((size_t)3 * capacity);
+        for (auto& e : G->tev) hip_check(hipEventCreate(&e), "hipEventCreate");
+        G->t_cap = capacity;
+        G->t_count = 0;
+    });
+}
+
+int qd_graph_read_timing(qd_graph* G, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        if (!n_calls) throw Fail(-91, "null n_calls");
+        const int n = std::min(G->t_count, std::max(0, max_calls));
+        for (int i = 0; i < n; ++i) {
+            hipEvent_t* e = &G->tev[(size_t)3 * i];
+            hip_check(hipEventSynchronize(e[2]), "hipEventSynchronize");
+            float t0 = 0, t1 = 0;
+            hip_check(hipEventElapsedTime(&t0, e[0], e[1]), "hipEventElapsedTime");
+            hip_check(hipEventElapsedTime(&t1, e[1], e[2]), "hipEventElapsedTime");
+            if (bp_ms) bp_ms[i] = t0;
+            if (ssf_ms) ssf_ms[i] = t1;
+        }
+        *n_calls = n;
+        G->t_count = 0;
     });
 }
 

@@ -424,20 +424,31 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
 template <typename T, int METHOD, int RC, int RV, int DRC>
 static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
-    if (!a.ssf)
-        return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, false>, lds, a.B, num_cus, stream, g, a);
+    if (!a.ssf) {
+        record_ev(a, 0, stream);
+        const int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, false>, lds, a.B, num_cus, stream, g, a);
+        record_ev(a, 1, stream);
+        record_ev(a, 2, stream);
+        return rc;
+    }
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
     if (e != hipSuccess) return (int)e;
+    record_ev(a, 0, stream);
     int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, true>, lds, a.B, num_cus, stream, g, a);
+    record_ev(a, 1, stream);
     if (rc != 0) return rc;
     if constexpr (RC <= 2) {
         if (g.n_gen <= g.m_pad && g.g_lc8) {  // register-cached tables: u8 ids, RC rounds of generators
             const size_t lds2 = (size_t)g.n_pad + 64 + (size_t)g.m_pad + 64;
-            return launch_persistent(ssf_wave_kernel<RC>, (lds2 + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+            rc = launch_persistent(ssf_wave_kernel<RC>, (lds2 + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+            record_ev(a, 2, stream);
+            return rc;
         }
     }
-    return launch_ssf_block(g, a, num_cus, stream);
+    rc = launch_ssf_block(g, a, num_cus, stream);
+    record_ev(a, 2, stream);
+    return rc;
 }
 
 template <typename T, int METHOD>

@@ -354,14 +354,23 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
         cap = (int)std::max<long long>(1, max_wg / num_cus);
     }
     T* gs = reinterpret_cast<T*>(scratch);
-    if (!a.ssf)
-        return launch_block(bp_block_kernel<T, METHOD, false>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+    if (!a.ssf) {
+        record_ev(a, 0, stream);
+        const int rc = launch_block(bp_block_kernel<T, METHOD, false>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+        record_ev(a, 1, stream);
+        record_ev(a, 2, stream);
+        return rc;
+    }
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
     if (e != hipSuccess) return (int)e;
+    record_ev(a, 0, stream);
     int rc = launch_block(bp_block_kernel<T, METHOD, true>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+    record_ev(a, 1, stream);
     if (rc != 0) return rc;
-    return launch_block2(ssf_block_kernel, small, a.B, num_cus, stream, g, a);
+    rc = launch_block2(ssf_block_kernel, small, a.B, num_cus, stream, g, a);
+    record_ev(a, 2, stream);
+    return rc;
 }
 
 size_t block_scratch_bytes(const DevGraph& g, int precision, int num_cus) {

@@ -94,7 +94,14 @@ struct DecodeArgs {
     int64_t* q_idx;    // [B]   shot of queue slot
     uint8_t* q_x;      // [B][n] BP hard decision
     uint8_t* q_r;      // [B][m] residual syndrome
+    // optional timing (host side only): events recorded on the launch stream
+    // before the BP kernel, after it, and after the SSF kernel
+    hipEvent_t* ev;    // [3] or nullptr
 };
+
+inline void record_ev(const DecodeArgs& a, int i, hipStream_t s) {
+    if (a.ev) (void)hipEventRecord(a.ev[i], s);
+}
 
 // Launchers (qdec_bp.hip / qdec_sample.hip).  Return hipError_t as int.
 int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a,

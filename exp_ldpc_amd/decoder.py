@@ -193,6 +193,23 @@ class Decoder:
             int(stream_id) & 0xFFFFFFFF, int(shot0), int(B), _abi.ptr(syn), _abi.ptr(readout), C.c_void_p(stream)),
             "qd_sample_storage_device")
 
+    # ------------------------------------------------------------ timing
+    def set_timing(self, capacity: int) -> None:
+        """Record HIP events around the BP and SSF kernels of the next
+        `capacity` decode calls (on their launch stream)."""
+        _abi.check(self._lib.qd_graph_set_timing(self._handle, int(capacity)), "qd_graph_set_timing")
+        self._t_cap = int(capacity)
+
+    def read_timing(self):
+        """(bp_ms[calls], ssf_ms[calls]) of the recorded calls; resets the ring."""
+        cap = getattr(self, "_t_cap", 0)
+        bp = np.zeros(max(cap, 1), np.float32)
+        ssf = np.zeros(max(cap, 1), np.float32)
+        cnt = C.c_int32(0)
+        _abi.check(self._lib.qd_graph_read_timing(self._handle, _abi.ptr(bp), _abi.ptr(ssf), cap, C.byref(cnt)),
+                   "qd_graph_read_timing")
+        return bp[:cnt.value].astype(np.float64), ssf[:cnt.value].astype(np.float64)
+
     def close(self) -> None:
         if getattr(self, "_handle", None) and self._handle.value:
             self._lib.qd_graph_destroy(self._handle)

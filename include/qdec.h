@@ -132,6 +132,15 @@ int qd_osd_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* co
                  uint8_t* osdw_out, int32_t nthreads);
 const char* qd_osd_last_error(void);
 
+/* Kernel timing for measurement: with capacity > 0, the next `capacity` decode
+ * calls record HIP events on their launch stream immediately before the BP kernel,
+ * after it and after the SSF kernel.  qd_graph_read_timing returns the per-call
+ * BP and SSF kernel durations (ms) and resets the ring.  No reference
+ * counterpart (the reference only reports whole-sweep walltime,
+ * misc/p_sweep.py:26-33). */
+int qd_graph_set_timing(qd_graph* g, int32_t capacity);
+int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
+
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */
 int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream);

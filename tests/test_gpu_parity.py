@@ -257,3 +257,24 @@ def test_spacetime_r2_fold(gpu_available, oracle_lib, code225):
                             lz=lz, readout=rd, want_llr=False)
     for key in ("corr", "iters", "status", "fail"):
         assert np.array_equal(got[key], ref[key]), key
+
+
+def test_kernel_timing_ring(gpu_available, oracle_lib, code225):
+    """qd_graph_set_timing/read_timing: one (BP, SSF) duration pair per decode
+    call up to the capacity; results unchanged by timing."""
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(77)
+    rd = _errors(rng, 4000, 225, 0.04)
+    syn = ((HZ @ rd.T).T % 2).astype(np.uint8)
+    dec = Decoder(HZ, 0.03, method="ms", precision="f32", max_iter=30, flip_sets=HX, logicals=code225.logicals.z)
+    base = dec.decode(syn, readout=rd, want=("x", "fail"))
+    dec.set_timing(2)
+    outs = [dec.decode(syn, readout=rd, want=("x", "fail")) for _ in range(3)]
+    bp, ssf = dec.read_timing()
+    assert bp.shape == (2,) and ssf.shape == (2,)
+    assert (bp > 0).all() and (ssf > 0).all()
+    for o in outs:
+        assert np.array_equal(o["x"], base["x"]) and np.array_equal(o["fail"], base["fail"])
+    assert dec.read_timing()[0].shape == (0,)
+    dec.set_timing(0)
+    dec.decode(syn, readout=rd, want=("fail",))
