@@ -146,6 +146,7 @@ def main():
     iters = torch.empty((nsteps, len(ps), B), dtype=torch.int32, device=dev)
     status = torch.empty((nsteps, len(ps), B), dtype=torch.uint8, device=dev)
     fail = torch.empty((nsteps, len(ps), B), dtype=torch.uint8, device=dev)
+    ssf_steps = torch.empty((nsteps, len(ps), B), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
@@ -153,7 +154,7 @@ def main():
     def step(s):
         for pi in range(len(ps)):
             decs[pi].decode_device(B, syn=syn[s, pi], readout=rd[s, pi], iters=iters[s, pi], status=status[s, pi],
-                                   fail=fail[s, pi], stream=stream.cuda_stream)
+                                   fail=fail[s, pi], ssf_steps=ssf_steps[s, pi], stream=stream.cuda_stream)
 
     for s in range(args.warmup):
         step(s)
@@ -194,6 +195,7 @@ def main():
     fails = fail[args.warmup:].to(torch.int64).sum(dim=(0, 2))
     conv = (status[args.warmup:] & 1).to(torch.int64).sum(dim=(0, 2))
     itp = iters[args.warmup:].to(torch.float64).mean(dim=(0, 2))
+    ssp = ssf_steps[args.warmup:].to(torch.float64).mean(dim=(0, 2))
     if world > 1:
         dist.all_reduce(fails)
         dist.all_reduce(conv)
@@ -211,6 +213,7 @@ def main():
                                "ler": float(fails[pi] / shots_per_point), "wilson95": [lo, hi],
                                "bp_converged_frac": float(conv[pi] / shots_per_point),
                                "mean_bp_iters_rank0": float(itp[pi]),
+                               "mean_ssf_steps_rank0": float(ssp[pi]),
                                "bp_kernel_ms_per_launch": float(bp_ms[:, pi].mean()),
                                "ssf_kernel_ms_per_launch": float(ssf_ms[:, pi].mean())}
         traffic = latest_traffic()

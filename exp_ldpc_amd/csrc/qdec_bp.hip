@@ -319,82 +319,182 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 }
 
 // ============================================================== SSF kernel
+// Four waves per workgroup share the generator tables in LDS; each wave
+// decodes its own queued shots independently (no cross-wave sync after the
+// table fill).  Incremental greedy: a generator's best score only changes when
+// its local syndrome changes, so every step
+//   1. lane l gathers the local syndromes (<= 32 bits) of generators l + 64 rg
+//      and compares them with the previous step's; changed generators with a
+//      non-zero local syndrome are compacted into a list (others score <= 0),
+//   2. the list is scored in chunks of 64 lanes (gen_best_score: 3 VALU per
+//      subset), each generator's key cached in LDS,
+//   3. a DPP wave max over the cached (score, -g) keys picks the generator, and
+//      the lowest subset reaching that score is found lane-parallel
+//      (spec: ties -> lowest g, then lowest subset bitmask),
+//   4. the flip updates the residual (u32 per check in LDS) and hard decision.
+// Key (int32): score << 15 | (127 - g) << 8; |score| <= 32*840 < 2^15, g < 128.
+constexpr int kSsfWaves = 4;
+
+// Orders this wave's LDS accesses across lanes: a wave's LDS operations execute
+// in issue order, so keeping the compiler from moving them is enough.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int RG>
-__global__ __launch_bounds__(64, 3) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
+struct SsfLds {
+    static constexpr int GP = 64 * RG;
+    __host__ __device__ static size_t shared_bytes() { return (size_t)GP * 4 * (kGenW + kGenLC / 4 + kGenW / 2); }
+    __host__ __device__ static size_t wave_bytes(const DevGraph& g) {
+        return (((size_t)g.m_pad + 64) * 4 + (size_t)GP * 4 * 2 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16;
+    }
+};
+
+template <int RG>
+__global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
+    constexpr int GP = SsfLds<RG>::GP;
+    constexpr int NLW = kGenLC / 4;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint8_t* xh = smem;                // [n_pad + 64]
-    uint8_t* sres = xh + g.n_pad + 64;  // [m_pad + 64], last 64 bytes stay 0 (pad ids)
-    const int lane = threadIdx.x;
+    // shared: qubit local-check masks, packed u8 local-check ids, packed u16 qubit ids
+    uint32_t* qmt = reinterpret_cast<uint32_t*>(smem);  // [kGenW][GP]
+    uint32_t* lct = qmt + kGenW * GP;                   // [NLW][GP]   (pad id m_pad -> zero residual)
+    uint32_t* qt = lct + NLW * GP;                      // [kGenW/2][GP]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned char* wbase = smem + SsfLds<RG>::shared_bytes() + (size_t)wave * SsfLds<RG>::wave_bytes(g);
+    uint32_t* sres = reinterpret_cast<uint32_t*>(wbase);      // [m_pad + 64] residual (pads stay 0)
+    int* key = reinterpret_cast<int*>(sres + g.m_pad + 64);   // [GP] cached best keys
+    uint32_t* slt = reinterpret_cast<uint32_t*>(key + GP);    // [GP] local syndromes of listed gens
+    uint8_t* list = reinterpret_cast<uint8_t*>(slt + GP);     // [GP] listed generators
+    uint8_t* xh = list + GP;                                  // [n_pad + 64]
     const int m = g.m, n = g.n;
 
-    // this lane's generators gi = rg*64 + lane: packed u8 local-check ids and
-    // per-qubit local-check masks (zero for qubits beyond the generator's weight)
-    uint32_t glc[RG][kGenLC / 4];
-    uint32_t gqm[RG][kGenW];
+    for (int e = threadIdx.x; e < GP; e += 64 * kSsfWaves) {
 #pragma unroll
-    for (int rg = 0; rg < RG; ++rg) {
-        const int gi = rg * 64 + lane;
+        for (int k = 0; k < kGenW; ++k) qmt[k * GP + e] = g.g_qmask[k * g.g_pad + e];
 #pragma unroll
-        for (int wq = 0; wq < kGenLC / 4; ++wq) glc[rg][wq] = g.g_lc8[wq * g.g_pad + gi];
+        for (int wq = 0; wq < NLW; ++wq) lct[wq * GP + e] = g.g_lc8[wq * g.g_pad + e];
 #pragma unroll
-        for (int k = 0; k < kGenW; ++k) gqm[rg][k] = g.g_qmask[k * g.g_pad + gi];
+        for (int k = 0; k < kGenW / 2; ++k)
+            qt[k * GP + e] = (uint32_t)g.g_q[(2 * k) * g.g_pad + e] | ((uint32_t)g.g_q[(2 * k + 1) * g.g_pad + e] << 16);
     }
-    for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
     for (int e = lane; e < g.m_pad + 64; e += 64) sres[e] = 0;
+    for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
     __syncthreads();
 
     const int count = *a.q_count;
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
     const int nlcw = (g.g_nlcmax + 3) / 4;
-    for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+    for (int slot = blockIdx.x * kSsfWaves + wave; slot < count; slot += gridDim.x * kSsfWaves) {
         const int64_t shot = a.q_idx[slot];
         for (int j = lane; j < n; j += 64) xh[j] = a.q_x[(int64_t)slot * n + j];
         int w_local = 0;
         for (int i = lane; i < m; i += 64) {
-            const uint8_t r = a.q_r[(int64_t)slot * m + i];
+            const uint32_t r = a.q_r[(int64_t)slot * m + i];
             sres[i] = r;
-            w_local += r;
+            w_local += (int)r;
         }
         int sw = wave_sum_i32(w_local);
-        __syncthreads();
+        wave_lds_sync();
+        uint32_t slo[RG];
         int steps = 0;
+        bool first = true;
         while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
-            long long best = LLONG_MIN;
+            // ---- 1. local syndromes; compact the changed, non-zero ones ----
+            int nl = 0;
 #pragma unroll
             for (int rg = 0; rg < RG; ++rg) {
                 const int gi = rg * 64 + lane;
-                uint32_t sl = 0;  // local syndrome of generator gi (pad ids -> zero bytes)
+                uint32_t sl = 0;
 #pragma unroll
-                for (int wq = 0; wq < kGenLC / 4; ++wq) {
+                for (int wq = 0; wq < NLW; ++wq) {
                     if (wq < nlcw) {
-                        const uint32_t pk = glc[rg][wq];
+                        const uint32_t pk = lct[wq * GP + gi];
 #pragma unroll
-                        for (int bb = 0; bb < 4; ++bb)
-                            sl |= (uint32_t)sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
+                        for (int bb = 0; bb < 4; ++bb) sl |= sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
                     }
                 }
-                if (__ballot(sl != 0u) == 0ull) continue;  // no positive gain in this round
-                best = max(best, gen_key64(gen_best_key(sl, gqm[rg], nhi), gi));
+                const bool changed = first || sl != slo[rg];
+                slo[rg] = sl;
+                const bool need = changed && sl != 0u;
+                if (changed && !need) key[gi] = INT_MIN;
+                const unsigned long long bal = __ballot(need);
+                if (need) {
+                    const int pos = nl + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    list[pos] = (uint8_t)gi;
+                    slt[pos] = sl;
+                }
+                nl += __popcll(bal);
             }
-            best = wave_max_i64(best);
-            const int score = (int)(best >> 32);
+            first = false;
+            wave_lds_sync();
+            // ---- 2. score the listed generators ----
+            for (int c0 = 0; c0 < nl; c0 += 64) {
+                const int idx = c0 + lane;
+                if (idx < nl) {
+                    const int gg = list[idx];
+                    const uint32_t sl = slt[idx];
+                    uint32_t qm[kGenW];
+#pragma unroll
+                    for (int k = 0; k < kGenW; ++k) qm[k] = qmt[k * GP + gg];
+                    const int sc = gen_best_score(sl, qm, nhi);
+                    key[gg] = (int)(((unsigned)sc << 15) | ((unsigned)(127 - gg) << 8));
+                }
+            }
+            wave_lds_sync();
+            // ---- 3. pick (score, -g), then the lowest subset reaching the score ----
+            int kv = INT_MIN;
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg) kv = max(kv, key[rg * 64 + lane]);
+            const int best = wave_max_i32(kv);
+            const int score = best >> 15;
             if (score <= 0) break;
-            const int gsel = 0xFFFFFF - (int)((best >> 8) & 0xFFFFFF);
-            const int tsel = 255 - (int)(best & 255);
+            const int gsel = 127 - ((best >> 8) & 127);
+            const int owner = gsel & 63, rsel = gsel >> 6;
+            uint32_t slg = 0;
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg)
+                if (rg == rsel) slg = (uint32_t)__builtin_amdgcn_readlane((int)slo[rg], owner);
+            const int base = __builtin_popcount(slg);
+            // lane k < kGenW holds qubit k's mask of the chosen generator
+            const uint32_t qk = lane < kGenW ? qmt[lane * GP + gsel] : 0u;
+            int tsel = -1;
+            for (int t0 = 0; t0 < 16 * nhi; t0 += 64) {
+                const int t = t0 + lane;
+                uint32_t mt = 0;
+#pragma unroll
+                for (int k = 0; k < kGenW; ++k) {
+                    const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)qk, k);
+                    mt ^= ((t >> k) & 1) ? q : 0u;
+                }
+                const int gain = base - __builtin_popcount(slg ^ mt);
+                const bool hit = t > 0 && t < 16 * nhi && gain * kSsfScale == score * __builtin_popcount(t);
+                const unsigned long long hb = __ballot(hit);
+                if (hb) {
+                    tsel = t0 + __builtin_ctzll(hb);
+                    break;
+                }
+            }
+            if (tsel < 0) break;  // unreachable: the best score is some subset's score
+            // ---- 4. apply the flip ----
+            const uint32_t fm = (uint32_t)wave_xor_masked(lane < kGenW && ((tsel >> lane) & 1) ? qk : 0u);
             const int gain = score * __builtin_popcount(tsel) / kSsfScale;
-            const int w = g.g_w[gsel];
-            uint32_t mask = 0;
-            for (int k = 0; k < w; ++k)
-                if ((tsel >> k) & 1) mask ^= g.g_qmask[k * g.g_pad + gsel];
-            if (lane < g.g_nlc[gsel] && ((mask >> lane) & 1)) sres[g.g_lc[lane * g.g_pad + gsel]] ^= 1;
-            if (lane < w && ((tsel >> lane) & 1)) xh[g.g_q[lane * g.g_pad + gsel]] ^= 1;
-            __syncthreads();
+            if (lane < kGenLC && ((fm >> lane) & 1)) {
+                const uint32_t wv = lct[(lane >> 2) * GP + gsel];
+                sres[(wv >> (8 * (lane & 3))) & 0xff] ^= 1u;
+            }
+            if (lane < kGenW && ((tsel >> lane) & 1)) {
+                const uint32_t qv = qt[(lane >> 1) * GP + gsel];
+                xh[(qv >> (16 * (lane & 1))) & 0xffff] ^= 1;
+            }
+            wave_lds_sync();
             sw -= gain;
             ++steps;
         }
         finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
-        for (int e = lane; e < g.m_pad; e += 64) sres[e] = 0;
-        __syncthreads();
+        wave_lds_sync();
     }
 }
 
@@ -405,6 +505,21 @@ static size_t wave_lds_bytes(const DevGraph& g) {
     constexpr int DCS = lds_stride<T, kDC>();
     return ((size_t)g.m_pad * DRS + 64) * sizeof(T) + ((size_t)g.n_pad * DCS + 64) * sizeof(T) +
            (size_t)g.n_pad + 64;
+}
+
+template <int RG>
+static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    const size_t lds = SsfLds<RG>::shared_bytes() + kSsfWaves * SsfLds<RG>::wave_bytes(g);
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ssf_wave_kernel<RG>, 64 * kSsfWaves, lds);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    long long grid = (long long)num_cus * per_cu;
+    const long long need = (a.B + kSsfWaves - 1) / kSsfWaves;  // queue length <= B
+    if (grid > need) grid = need;
+    if (grid <= 0) return 0;
+    hipLaunchKernelGGL(ssf_wave_kernel<RG>, dim3((unsigned)grid), dim3(64 * kSsfWaves), lds, stream, g, a);
+    return (int)hipGetLastError();
 }
 
 template <typename K>
@@ -438,13 +553,10 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipS
     int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, true>, lds, a.B, num_cus, stream, g, a);
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
-    if constexpr (RC <= 2) {
-        if (g.n_gen <= g.m_pad && g.g_lc8) {  // register-cached tables: u8 ids, RC rounds of generators
-            const size_t lds2 = (size_t)g.n_pad + 64 + (size_t)g.m_pad + 64;
-            rc = launch_persistent(ssf_wave_kernel<RC>, (lds2 + 15) / 16 * 16, a.B, num_cus, stream, g, a);
-            record_ev(a, 2, stream);
-            return rc;
-        }
+    if (g.n_gen <= 128 && g.g_lc8) {  // register-owned generators, u8 local-check ids
+        rc = g.n_gen <= 64 ? launch_ssf_wave<1>(g, a, num_cus, stream) : launch_ssf_wave<2>(g, a, num_cus, stream);
+        record_ev(a, 2, stream);
+        return rc;
     }
     rc = launch_ssf_block(g, a, num_cus, stream);
     record_ev(a, 2, stream);

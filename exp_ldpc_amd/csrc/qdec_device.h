@@ -99,6 +99,68 @@ __device__ __forceinline__ int gen_best_key(uint32_t sl, const uint32_t (&qm)[kG
     return best32;
 }
 
+// Wave-wide max of an int with DPP row shifts and row broadcasts (VALU only, no
+// LDS round trips): inclusive max-scan within each 16-lane row, then rows 0-1
+// and 2-3 via row_bcast:15, then all four via row_bcast:31; lane 63 holds the
+// result.  All 64 lanes must be active.
+__device__ __forceinline__ int wave_max_i32(int v) {
+#define QDEC_DPP_MAX(ctrl, rm, bm) v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, ctrl, rm, bm, false))
+    QDEC_DPP_MAX(0x111, 0xf, 0xf);  // row_shr:1
+    QDEC_DPP_MAX(0x112, 0xf, 0xf);  // row_shr:2
+    QDEC_DPP_MAX(0x114, 0xf, 0xf);  // row_shr:4
+    QDEC_DPP_MAX(0x118, 0xf, 0xf);  // row_shr:8
+    QDEC_DPP_MAX(0x142, 0xa, 0xf);  // row_bcast:15 -> rows 1, 3
+    QDEC_DPP_MAX(0x143, 0xc, 0xf);  // row_bcast:31 -> rows 2, 3
+#undef QDEC_DPP_MAX
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// XOR over lanes 0..7 of v (other lanes must pass 0), result in every lane.
+__device__ __forceinline__ int wave_xor_masked(int v) {
+    v ^= __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v ^= __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v ^= __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    return __builtin_amdgcn_readlane(v, 7);
+}
+
+// Best small-set-flip SCORE of one generator (the subset itself is recovered
+// afterwards, for the winning generator only; ssf_pick_subset).  For every
+// subset size d the minimum residual weight popc(sl ^ M_t) over |t| = d is kept
+// (3 VALU per subset: xor, popcount, min), then score = max_d (popc(sl) -
+// min_d) * 840/d.  Subsets using qubits beyond the generator's weight have zero
+// masks and a larger |t| than the same subset without them, so they never
+// raise the maximum of a positive score.  nhi = 2^(wmax-4) blocks of 16.
+__device__ __forceinline__ int gen_best_score(uint32_t sl, const uint32_t (&qm)[kGenW], int nhi) {
+    const int base = __builtin_popcount(sl);
+    uint32_t lo[16];
+    lo[0] = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
+    uint32_t mn[kGenW + 1];
+#pragma unroll
+    for (int d = 0; d <= kGenW; ++d) mn[d] = 64u;
+#pragma unroll
+    for (int hi = 0; hi < 16; ++hi) {
+        if (hi < nhi) {  // uniform
+            uint32_t mh = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+                if ((hi >> bb) & 1) mh ^= qm[4 + bb];
+            const uint32_t sh = sl ^ mh;
+#pragma unroll
+            for (int l = 0; l < 16; ++l) {
+                if (hi == 0 && l == 0) continue;  // empty set
+                const int d = __builtin_popcount(hi) + __builtin_popcount(l);
+                mn[d] = min(mn[d], (uint32_t)__builtin_popcount(sh ^ lo[l]));
+            }
+        }
+    }
+    int best = INT_MIN;
+#pragma unroll
+    for (int d = 1; d <= kGenW; ++d) best = max(best, (base - (int)mn[d]) * (840 / d));
+    return best;
+}
+
 // (score, -g, -t) packed so that a signed max picks the spec's winner.
 __device__ __forceinline__ long long gen_key64(int best32, int gi) {
     return ((long long)(best32 >> 8) << 32) | ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);
