@@ -10,6 +10,7 @@ denormals kept.
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -19,7 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libqdec_hip.so")
 SOURCES = ["qdec_abi.cpp", "qdec_osd.cpp", "qdec_bp.hip", "qdec_bp_block.hip", "qdec_sample.hip"]
-HEADERS = ["qdec_internal.h", "qdec_device.h", os.path.join("..", "..", "include", "qdec.h")]
+HEADERS = [os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.h"))] + ["../../include/qdec.h"]
 ARCH = os.environ.get("QDEC_OFFLOAD_ARCH", "gfx950")
 
 FLAGS = [

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <random>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -100,6 +101,119 @@ template <typename T>
 int dcs() { return lds_stride<T, kDC>(); }
 
 void set_device(qd_graph* g) { hip_check(hipSetDevice(g->device), "hipSetDevice"); }
+
+// Layout of the compressed-state min-sum kernel (qdec_bp_ms.h).  Variable
+// lane j = rv*64 + l scatters its k-th v2c message to element i*DRS + pos of
+// check i's row.  One ds_write_b32 per (rv, k) serves 2 x 32 lanes, bank =
+// dword % 32.  It costs max(4, L0 + L1) cycles, where L_h is the worst bank
+// load in half h.  The check pass takes min/sign over the whole row, which is
+// independent of the row order, so edge positions inside a row are free.  A
+// seeded hill climb over position swaps drives every instruction to <= 2-way
+// conflicts (tie-break: sum of squared loads).  Pad lanes of an instruction all
+// write one dummy element, placed in the least-loaded bank.
+void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
+    DevGraph& g = G->dg;
+    const auto& rp = G->row_ptr;
+    const auto& ci = G->col_idx;
+    const int E = rp[m];
+    const int drc = g.shape_drc;
+    const int RVn = g.n_pad / 64;
+    const int DRSf = drs<float>();
+    // edge e (CSR order): group (rv, k), half, lane
+    std::vector<int> grp(E), half(E), pos(E);
+    for (int i = 0; i < m; ++i)
+        for (int e = rp[i], t = 0; e < rp[i + 1]; ++e, ++t) {
+            const int j = ci[e];
+            grp[e] = (j / 64) * kDC + edge_cpos[e];
+            half[e] = (j % 64) / 32;
+            pos[e] = t;
+        }
+    const int NG = RVn * kDC;
+    std::vector<int> load((size_t)NG * 2 * 32, 0);
+    auto bank = [&](int e, int i) { return (i * DRSf + pos[e]) % 32; };
+    std::vector<int> row_of(E);
+    for (int i = 0; i < m; ++i)
+        for (int e = rp[i]; e < rp[i + 1]; ++e) row_of[e] = i;
+    for (int e = 0; e < E; ++e) load[((size_t)grp[e] * 2 + half[e]) * 32 + bank(e, row_of[e])]++;
+    auto gcost = [&](int gi) {
+        int mx[2] = {0, 0}, sq = 0;
+        for (int h = 0; h < 2; ++h)
+            for (int b = 0; b < 32; ++b) {
+                const int v = load[((size_t)gi * 2 + h) * 32 + b];
+                mx[h] = std::max(mx[h], v);
+                sq += v * v;
+            }
+        return (long)std::max(4, mx[0] + mx[1]) * 100000 + sq;
+    };
+    std::mt19937 rng(12345);
+    // free positions of each row (rows shorter than drc)
+    for (int iter = 0; iter < 40 * E; ++iter) {
+        const int i = (int)(rng() % (unsigned)m);
+        const int deg = rp[i + 1] - rp[i];
+        if (deg < 1) continue;
+        const int e1 = rp[i] + (int)(rng() % (unsigned)deg);
+        const int p2 = (int)(rng() % (unsigned)drc);
+        int e2 = -1;
+        for (int e = rp[i]; e < rp[i + 1]; ++e)
+            if (pos[e] == p2) e2 = e;
+        if (e2 == e1) continue;
+        const int g1 = grp[e1], g2 = e2 >= 0 ? grp[e2] : -1;
+        const long before = gcost(g1) + (g2 >= 0 && g2 != g1 ? gcost(g2) : 0);
+        auto move = [&](int e, int newpos) {
+            load[((size_t)grp[e] * 2 + half[e]) * 32 + bank(e, i)]--;
+            pos[e] = newpos;
+            load[((size_t)grp[e] * 2 + half[e]) * 32 + bank(e, i)]++;
+        };
+        const int p1 = pos[e1];
+        move(e1, p2);
+        if (e2 >= 0) move(e2, p1);
+        const long after = gcost(g1) + (g2 >= 0 && g2 != g1 ? gcost(g2) : 0);
+        if (after > before) {  // undo
+            if (e2 >= 0) move(e2, p2);
+            move(e1, p1);
+        }
+    }
+    // dummy element per group, in the bank least loaded over the halves with pads
+    std::vector<int> dummy_bank(NG, 0);
+    for (int gi = 0; gi < NG; ++gi) {
+        const int rv = gi / kDC, k = gi % kDC;
+        bool pads[2] = {false, false};
+        for (int l = 0; l < 64; ++l) {
+            const int j = rv * 64 + l;
+            if (j >= n || k >= G->col_ptr[j + 1] - G->col_ptr[j]) pads[l / 32] = true;
+        }
+        int bestb = 0, bestc = 1 << 30;
+        for (int b = 0; b < 32; ++b) {
+            int c = 0;
+            for (int h = 0; h < 2; ++h)
+                if (pads[h]) c = std::max(c, load[((size_t)gi * 2 + h) * 32 + b]);
+            if (c < bestc) { bestc = c; bestb = b; }
+        }
+        dummy_bank[gi] = bestb;
+    }
+    const int DRS[2] = {drs<double>(), drs<float>()};
+    for (int p = 0; p < 2; ++p) {
+        std::vector<uint32_t> etab((size_t)kDC * g.n_pad);
+        const int dstart = g.m_pad * DRS[p];
+        for (int gi = 0; gi < NG; ++gi) {
+            const int rv = gi / kDC, k = gi % kDC;
+            // element whose first dword lands in the chosen bank
+            const int dw0 = dstart * (p == 0 ? 2 : 1);
+            const int d = p == 0 ? ((dummy_bank[gi] - dw0 % 32 + 32) % 32) / 2 : (dummy_bank[gi] - dw0 % 32 + 32) % 32;
+            for (int l = 0; l < 64; ++l)
+                etab[(size_t)k * g.n_pad + rv * 64 + l] = (uint32_t)(dstart + d) | ((uint32_t)g.m_pad << 16);
+        }
+        for (int i = 0; i < m; ++i)
+            for (int e = rp[i]; e < rp[i + 1]; ++e)
+                etab[(size_t)edge_cpos[e] * g.n_pad + ci[e]] = (uint32_t)(i * DRS[p] + pos[e]) | ((uint32_t)i << 16);
+        g.ms_etab[p] = G->arena.upload(etab);
+    }
+    const int W = g.n_pad / 64;
+    std::vector<uint64_t> smask((size_t)W * g.m_pad, 0);
+    for (int i = 0; i < m; ++i)
+        for (int e = rp[i]; e < rp[i + 1]; ++e) smask[(size_t)(ci[e] / 64) * g.m_pad + i] ^= 1ull << (ci[e] % 64);
+    g.ms_smask = G->arena.upload(smask);
+}
 
 void build_tables(qd_graph* G, int m, int n) {
     DevGraph& g = G->dg;
@@ -196,6 +310,7 @@ void build_tables(qd_graph* G, int m, int n) {
     }
     g.row_ptr = G->arena.upload(G->row_ptr);
     g.col_idx = G->arena.upload(G->col_idx);
+    ms_layout(G, m, n, edge_cpos);
 }
 
 // Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.

@@ -37,53 +37,9 @@
 #include <hip/hip_runtime.h>
 
 #include "qdec_device.h"
+#include "qdec_bp_ms.h"
 
 namespace qdec {
-
-constexpr int kMaxLogicalRounds = 4;  // k <= 256 logicals in the fused check
-
-// Final per-shot outputs from the hard decision in LDS: x_out, corr = base ^
-// fold(x), fail = any_r parity(lz[r] & (readout ^ corr)), status, ssf_steps.
-__device__ void finalize_shot(const DevGraph& g, const DecodeArgs& a, int64_t shot, const uint8_t* xh,
-                              bool conv, bool satisfied, int steps, int lane) {
-    const int n = g.n;
-    if (a.x_out)
-        for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
-    const bool want_fail = a.fail && a.readout && g.k > 0;
-    int lpar[kMaxLogicalRounds] = {0, 0, 0, 0};
-    if (a.corr_out || want_fail) {
-        for (int w0 = 0; w0 < g.lz_words; ++w0) {
-            const int q = w0 * 64 + lane;
-            int cb = 0;
-            if (q < g.n_data) {
-                cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
-                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
-                if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
-            }
-            if (want_fail) {
-                const int v = (q < g.n_data) ? ((a.readout[shot * g.n_data + q] ^ cb) & 1) : 0;
-                const unsigned long long word = __ballot(v);
-#pragma unroll
-                for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
-                    const int r = rr * 64 + lane;
-                    if (r < g.k) lpar[rr] ^= __popcll(g.lz[(size_t)r * g.lz_words + w0] & word) & 1;
-                }
-            }
-        }
-    }
-    int any_fail = 0;
-    if (want_fail) {
-        int f = 0;
-#pragma unroll
-        for (int rr = 0; rr < kMaxLogicalRounds; ++rr) f |= lpar[rr];
-        any_fail = __ballot(f) != 0ull;
-    }
-    if (lane == 0) {
-        if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
-        if (a.ssf_steps) a.ssf_steps[shot] = steps;
-        if (a.fail) a.fail[shot] = (uint8_t)any_fail;
-    }
-}
 
 // ============================================================== BP kernel
 template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
@@ -536,12 +492,24 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
     return (int)hipGetLastError();
 }
 
+// BP kernel of a wave shape: min-sum uses the compressed-state kernel, product-sum
+// the message-array kernel.
+template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
+static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    if constexpr (METHOD == 1) {
+        const size_t lds = MsLds<T>::bytes(g.m_pad, g.n_pad);
+        return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER>, lds, a.B, num_cus, stream, g, a);
+    } else {
+        const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
+        return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, DEFER>, lds, a.B, num_cus, stream, g, a);
+    }
+}
+
 template <typename T, int METHOD, int RC, int RV, int DRC>
 static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
-    const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
     if (!a.ssf) {
         record_ev(a, 0, stream);
-        const int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, false>, lds, a.B, num_cus, stream, g, a);
+        const int rc = launch_bp_wave<T, METHOD, RC, RV, DRC, false>(g, a, num_cus, stream);
         record_ev(a, 1, stream);
         record_ev(a, 2, stream);
         return rc;
@@ -550,7 +518,7 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipS
     hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
     if (e != hipSuccess) return (int)e;
     record_ev(a, 0, stream);
-    int rc = launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, true>, lds, a.B, num_cus, stream, g, a);
+    int rc = launch_bp_wave<T, METHOD, RC, RV, DRC, true>(g, a, num_cus, stream);
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
     if (g.n_gen <= 128 && g.g_lc8) {  // register-owned generators, u8 local-check ids

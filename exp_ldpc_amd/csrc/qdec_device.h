@@ -166,4 +166,49 @@ __device__ __forceinline__ long long gen_key64(int best32, int gi) {
     return ((long long)(best32 >> 8) << 32) | ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);
 }
 
+constexpr int kMaxLogicalRounds = 4;  // k <= 256 logicals in the fused check
+
+// Final per-shot outputs from the hard decision in LDS: x_out, corr = base ^
+// fold(x), fail = any_r parity(lz[r] & (readout ^ corr)), status, ssf_steps.
+__device__ inline void finalize_shot(const DevGraph& g, const DecodeArgs& a, int64_t shot, const uint8_t* xh,
+                              bool conv, bool satisfied, int steps, int lane) {
+    const int n = g.n;
+    if (a.x_out)
+        for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    int lpar[kMaxLogicalRounds] = {0, 0, 0, 0};
+    if (a.corr_out || want_fail) {
+        for (int w0 = 0; w0 < g.lz_words; ++w0) {
+            const int q = w0 * 64 + lane;
+            int cb = 0;
+            if (q < g.n_data) {
+                cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
+                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+                if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+            }
+            if (want_fail) {
+                const int v = (q < g.n_data) ? ((a.readout[shot * g.n_data + q] ^ cb) & 1) : 0;
+                const unsigned long long word = __ballot(v);
+#pragma unroll
+                for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                    const int r = rr * 64 + lane;
+                    if (r < g.k) lpar[rr] ^= __popcll(g.lz[(size_t)r * g.lz_words + w0] & word) & 1;
+                }
+            }
+        }
+    }
+    int any_fail = 0;
+    if (want_fail) {
+        int f = 0;
+#pragma unroll
+        for (int rr = 0; rr < kMaxLogicalRounds; ++rr) f |= lpar[rr];
+        any_fail = __ballot(f) != 0ull;
+    }
+    if (lane == 0) {
+        if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
+        if (a.ssf_steps) a.ssf_steps[shot] = steps;
+        if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+    }
+}
+
 }  // namespace qdec

@@ -61,6 +61,13 @@ struct DevGraph {
     const int32_t* col_idx;
     const int32_t* col_ptr;       // [n+1]
     const int32_t* col_edge;      // [E] CSR edge ids of column j, ascending row
+    // min-sum wave kernel with compressed check state (qdec_bp_ms.h): variable
+    // edge k scatters its v2c message to element (etab & 0xffff) and gathers
+    // check state (etab >> 16); pads -> a dummy element / the zero state m_pad.
+    // Row positions inside a check's v2c row are chosen on the host so the
+    // scatter has at most 2-way bank conflicts (ms_layout in qdec_abi.cpp).
+    const uint32_t* ms_etab[2];   // [kDC][n_pad], per precision (element strides differ)
+    const uint64_t* ms_smask;     // [n_pad/64][m_pad] columns of check i inside 64-column word w
     // flip sets (SSF)
     int n_gen, g_pad, g_wmax;
     const uint8_t* g_w;           // [g_pad]
