@@ -45,11 +45,15 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    """Build the library; stamps=True builds the development variant with phase
+    timers (libqdec_hip_stamps.so, loaded with QDEC_LIB=...)."""
+    lib = LIB.replace(".so", "_stamps.so") if stamps else LIB
+    if not force and not stamps and not _stale():
         return LIB
-    tmp = LIB + ".tmp"
-    cmd = [_hipcc(), *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
+    tmp = lib + ".tmp"
+    extra = ["-DQDEC_STAMPS"] if stamps else []
+    cmd = [_hipcc(), *FLAGS, *extra, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -57,9 +61,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-6000:]}")
     if verbose and res.stderr:
         print(res.stderr[-4000:], file=sys.stderr)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <random>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -91,6 +92,8 @@ struct qd_graph {
     // kernel timing ring (qd_graph_set_timing): 3 events per decode call
     std::vector<hipEvent_t> tev;
     int t_cap = 0, t_count = 0;
+    // min-sum wave kernel: variable (column) held by each lane slot, -1 for pads
+    std::vector<int> ms_var_of_slot;
 };
 
 namespace {
@@ -119,13 +122,36 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
     const int drc = g.shape_drc;
     const int RVn = g.n_pad / 64;
     const int DRSf = drs<float>();
+    // Lane slots of the variables: ascending column degree (stable), so the
+    // leading 64-variable rounds whose variables all have degree <= 3 run a
+    // 3-edge variable pass (ms_d3r).  Each variable's arithmetic is unchanged.
+    std::vector<int> order(n);
+    for (int j = 0; j < n; ++j) order[j] = j;
+    auto cdeg = [&](int j) { return G->col_ptr[j + 1] - G->col_ptr[j]; };
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cdeg(x) < cdeg(y); });
+    std::vector<int> slot_of(n);
+    G->ms_var_of_slot.assign(g.n_pad, -1);
+    for (int s2 = 0; s2 < n; ++s2) {
+        slot_of[order[s2]] = s2;
+        G->ms_var_of_slot[s2] = order[s2];
+    }
+    g.ms_d3r = 0;
+    for (int r = 0; r < RVn; ++r) {
+        bool ok = true;
+        for (int l = 0; l < 64; ++l) {
+            const int j = G->ms_var_of_slot[r * 64 + l];
+            if (j >= 0 && cdeg(j) > 3) ok = false;
+        }
+        if (!ok) break;
+        g.ms_d3r = r + 1;
+    }
     // edge e (CSR order): group (rv, k), half, lane
     std::vector<int> grp(E), half(E), pos(E);
     for (int i = 0; i < m; ++i)
         for (int e = rp[i], t = 0; e < rp[i + 1]; ++e, ++t) {
-            const int j = ci[e];
-            grp[e] = (j / 64) * kDC + edge_cpos[e];
-            half[e] = (j % 64) / 32;
+            const int sl = slot_of[ci[e]];
+            grp[e] = (sl / 64) * kDC + edge_cpos[e];
+            half[e] = (sl % 64) / 32;
             pos[e] = t;
         }
     const int NG = RVn * kDC;
@@ -179,8 +205,8 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
         const int rv = gi / kDC, k = gi % kDC;
         bool pads[2] = {false, false};
         for (int l = 0; l < 64; ++l) {
-            const int j = rv * 64 + l;
-            if (j >= n || k >= G->col_ptr[j + 1] - G->col_ptr[j]) pads[l / 32] = true;
+            const int j = G->ms_var_of_slot[rv * 64 + l];
+            if (j < 0 || k >= cdeg(j)) pads[l / 32] = true;
         }
         int bestb = 0, bestc = 1 << 30;
         for (int b = 0; b < 32; ++b) {
@@ -205,13 +231,22 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
         }
         for (int i = 0; i < m; ++i)
             for (int e = rp[i]; e < rp[i + 1]; ++e)
-                etab[(size_t)edge_cpos[e] * g.n_pad + ci[e]] = (uint32_t)(i * DRS[p] + pos[e]) | ((uint32_t)i << 16);
+                etab[(size_t)edge_cpos[e] * g.n_pad + slot_of[ci[e]]] =
+                    (uint32_t)(i * DRS[p] + pos[e]) | ((uint32_t)i << 16);
         g.ms_etab[p] = G->arena.upload(etab);
     }
+    // column of each slot (pads: a per-lane dummy past n_pad in the kernel's xh)
+    std::vector<uint16_t> vsl(g.n_pad);
+    for (int s2 = 0; s2 < g.n_pad; ++s2)
+        vsl[s2] = (uint16_t)(G->ms_var_of_slot[s2] >= 0 ? G->ms_var_of_slot[s2] : g.n_pad + s2 % 64);
+    g.ms_vslot = G->arena.upload(vsl);
     const int W = g.n_pad / 64;
     std::vector<uint64_t> smask((size_t)W * g.m_pad, 0);
     for (int i = 0; i < m; ++i)
-        for (int e = rp[i]; e < rp[i + 1]; ++e) smask[(size_t)(ci[e] / 64) * g.m_pad + i] ^= 1ull << (ci[e] % 64);
+        for (int e = rp[i]; e < rp[i + 1]; ++e) {
+            const int sl = slot_of[ci[e]];
+            smask[(size_t)(sl / 64) * g.m_pad + i] ^= 1ull << (sl % 64);
+        }
     g.ms_smask = G->arena.upload(smask);
 }
 
@@ -576,6 +611,19 @@ int qd_graph_set_priors(qd_graph* G, const double* probs) {
         G->prior_arena.release();
         g.prior[QD_MIN_SUM][QD_F64] = G->prior_arena.upload(ms64);
         g.prior[QD_MIN_SUM][QD_F32] = G->prior_arena.upload(ms32);
+        if (!G->ms_var_of_slot.empty()) {  // min-sum wave kernel: lane-slot order
+            std::vector<double> s64(g.n_pad, 0.0);
+            std::vector<float> s32(g.n_pad, 0.0f);
+            for (int s2 = 0; s2 < g.n_pad; ++s2) {
+                const int j = G->ms_var_of_slot[s2];
+                if (j >= 0) {
+                    s64[s2] = ms64[j];
+                    s32[s2] = ms32[j];
+                }
+            }
+            g.ms_prior[QD_F64] = G->prior_arena.upload(s64);
+            g.ms_prior[QD_F32] = G->prior_arena.upload(s32);
+        }
         g.prior[QD_PRODUCT_SUM][QD_F64] = G->prior_arena.upload(ps64);
         g.prior[QD_PRODUCT_SUM][QD_F32] = G->prior_arena.upload(ps32);
         G->has_priors = true;

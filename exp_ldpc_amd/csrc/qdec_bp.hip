@@ -291,14 +291,6 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 // Key (int32): score << 15 | (127 - g) << 8; |score| <= 32*840 < 2^15, g < 128.
 constexpr int kSsfWaves = 4;
 
-// Orders this wave's LDS accesses across lanes: a wave's LDS operations execute
-// in issue order, so keeping the compiler from moving them is enough.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <int RG>
 struct SsfLds {
     static constexpr int GP = 64 * RG;
@@ -480,15 +472,15 @@ static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, 
 
 template <typename K>
 static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
-                             const DecodeArgs& a) {
+                             const DecodeArgs& a, int block = 64) {
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
     long long grid = (long long)num_cus * per_cu;
     if (grid > work) grid = work;
     if (grid <= 0) return 0;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, stream, g, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), lds, stream, g, a);
     return (int)hipGetLastError();
 }
 
@@ -497,8 +489,21 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
 template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
 static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if constexpr (METHOD == 1) {
-        const size_t lds = MsLds<T>::bytes(g.m_pad, g.n_pad);
-        return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER>, lds, a.B, num_cus, stream, g, a);
+        const size_t lds = MsLds<T>::template bytes<RC, RV>(g);
+        const bool lean = !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1;
+        // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
+        if constexpr (RC == 2 && RV == 4 && DRC == 7) {
+            if (g.ms_d3r >= 2) {
+                if (lean)
+                    return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 2>, lds, a.B, num_cus,
+                                             stream, g, a);
+                return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 2>, lds, a.B, num_cus,
+                                         stream, g, a);
+            }
+        }
+        if (lean)
+            return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 0>, lds, a.B, num_cus, stream, g, a);
+        return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 0>, lds, a.B, num_cus, stream, g, a);
     } else {
         const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
         return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, DEFER>, lds, a.B, num_cus, stream, g, a);
@@ -560,6 +565,19 @@ int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs
     return method == 1 ? dispatch_shape<double, 1>(g, a, num_cus, stream)
                        : dispatch_shape<double, 0>(g, a, num_cus, stream);
 }
+
+#ifdef QDEC_STAMPS
+extern "C" __attribute__((visibility("default"))) int qd_dev_read_stamps(unsigned long long* out, int n, int reset) {
+    unsigned long long h[64] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(qdec_stamps), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < 64; ++i) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[64] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(qdec_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------- flag counter
 __global__ void count_flags_kernel(const uint8_t* __restrict__ f, int64_t B, uint8_t mask,

@@ -13,10 +13,13 @@
 //   check pass  RC x (ds_read_b128 x2 row + ds_write_b64 state)
 //   var pass    RV x 4 x (ds_read_b64 state gather + ds_write_b32 v2c scatter)
 // The syndrome test needs no LDS at all.  Hard decisions are ballots
-// (X[w] = 64 columns per word), and check i's parity is
-// popc(X & smask_i) mod 2 with per-lane column masks.  The host picks v2c row
-// positions (qdec_abi.cpp ms_layout) so each scatter instruction has at most
-// 2-way bank conflicts, which ds_write_b32 absorbs for free.
+// (X[w] = 64 lane slots per word), and check i's parity is
+// popc(X & smask_i) mod 2 with per-lane slot masks.  The host (qdec_abi.cpp
+// ms_layout) places variables in lane slots by ascending degree, so the
+// leading all-degree-3 rounds (D3R) run a 3-edge variable pass.  It also picks
+// v2c row positions so each scatter instruction has at most 2-way bank
+// conflicts, which ds_write_b32 absorbs for free.  Shot inputs are staged
+// through LDS one shot ahead (ShotIo).
 #pragma once
 
 namespace qdec {
@@ -44,37 +47,66 @@ struct MsLds {
     __host__ __device__ static size_t state_elems(int m_pad) {
         return ((size_t)2 * (m_pad + 1) * sizeof(T) + 15) / 16 * 16 / sizeof(T);
     }
-    __host__ __device__ static size_t bytes(int m_pad, int n_pad) {
+    __host__ __device__ static size_t core_bytes(int m_pad, int n_pad) {
         return ((v2c_elems(m_pad) + state_elems(m_pad)) * sizeof(T) + (size_t)n_pad + 64 + 15) / 16 * 16;
+    }
+    template <int RC, int RV>
+    __host__ __device__ static size_t bytes(const DevGraph& g) {
+        return core_bytes(g.m_pad, g.n_pad) + ShotIo<RC, RV>::bytes(g);
     }
 };
 
-template <typename T, int RC, int RV, int DRC, bool DEFER>
+// alpha_t = 1 - 2^-t (ms_scaling == 0) built from bits on the scalar unit:
+// 1 - 2^-t is 1.0 minus 2^(P-t) units in the last place below 1.0 (P = 24 for
+// float, 53 for double), and rounds to 1.0 for t > P, exactly as
+// (T)(1.0 - ldexp(1.0, -t)) does.
+template <typename T>
+__device__ __forceinline__ T alpha_bits(int it, double ms_scaling) {
+    if (ms_scaling != 0.0) return (T)ms_scaling;
+    if constexpr (sizeof(T) == 4) {
+        const uint32_t u = 0x3F800000u - (it <= 24 ? (1u << (24 - it)) : 0u);
+        return __uint_as_float(u);
+    } else {
+        const unsigned long long u = 0x3FF0000000000000ull - (it <= 53 ? (1ull << (53 - it)) : 0ull);
+        return __longlong_as_double((long long)u);
+    }
+}
+
+// LEAN: the throughput configuration (no x / corr / llr outputs, no base, no
+// syndrome flags, no spacetime fold): the per-shot epilogue is the ballot-word
+// failure check only, which keeps the kernel's scalar state small.
+// D3R: leading variable rounds whose slots all have degree <= 3.
+template <typename T, int RC, int RV, int DRC, bool DEFER, bool LEAN, int D3R>
 __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArgs a) {
     static_assert(DRC <= kDR, "compute width exceeds the LDS row");
-    using U = typename FBits<T>::U;
+    static_assert(D3R <= RV, "degree rounds");
     using V2 = __attribute__((ext_vector_type(2))) T;
+    using Io = ShotIo<RC, RV>;
     constexpr int DRS = MsLds<T>::DRS;
     constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
-    constexpr U kSign = (U)1 << (8 * sizeof(T) - 1);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* v2c = reinterpret_cast<T*>(smem);
     T* st = v2c + MsLds<T>::v2c_elems(g.m_pad);
     uint8_t* xh = reinterpret_cast<uint8_t*>(st + MsLds<T>::state_elems(g.m_pad));
+    Io io(g, smem + MsLds<T>::core_bytes(g.m_pad, g.n_pad));
 
     const int lane = threadIdx.x;
     const int m = g.m, n = g.n;
-    const T* prior = reinterpret_cast<const T*>(g.prior[1][PREC]);
+    const T* prior = reinterpret_cast<const T*>(g.ms_prior[PREC]);
 
-    uint32_t etab[RV][kDC];  // v2c element | state index << 16
+    uint32_t etab[RV][kDC];  // v2c element | state index << 16 (edges k < kd(rv))
     T L[RV];
+    uint32_t vsl[(RV + 1) / 2];  // columns of this lane's slots, u16 pairs
 #pragma unroll
     for (int rv = 0; rv < RV; ++rv) {
-        const int j = rv * 64 + lane;
-        L[rv] = prior[j];
+        const int sl = rv * 64 + lane;
+        L[rv] = prior[sl];
 #pragma unroll
-        for (int k = 0; k < kDC; ++k) etab[rv][k] = g.ms_etab[PREC][k * g.n_pad + j];
+        for (int k = 0; k < kDC; ++k) etab[rv][k] = (rv < D3R && k == 3) ? 0u : g.ms_etab[PREC][k * g.n_pad + sl];
+        if (rv % 2 == 0) vsl[rv / 2] = g.ms_vslot[sl];
+        else vsl[rv / 2] |= (uint32_t)g.ms_vslot[sl] << 16;
     }
+    auto col_of = [&](int rv) -> int { return (int)((vsl[rv / 2] >> (16 * (rv % 2))) & 0xffffu); };
     uint64_t smask[RC][RV];
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc)
@@ -86,23 +118,39 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
     for (int e = lane; e < (int)MsLds<T>::v2c_elems(g.m_pad); e += 64) v2c[e] = Big<T>::v;
     for (int e = lane; e < (int)MsLds<T>::state_elems(g.m_pad); e += 64) st[e] = (T)0;
     for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
-    __syncthreads();
+    io.init(g, lane);
+    io.stage(g, a, blockIdx.x, 0, lane);
+    wave_lds_sync();
 
-    for (int64_t shot = blockIdx.x; shot < a.B; shot += gridDim.x) {
-        // ---- syndrome ----
+    int buf = 0;
+    QDEC_STAMP_DECL
+#ifdef QDEC_STAMPS
+    const unsigned long long qdec_t0 = __builtin_amdgcn_s_memtime(), qdec_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (int64_t shot = blockIdx.x; shot < a.B; shot += gridDim.x, buf ^= 1) {
+        // ---- syndrome (staged one shot ahead: at least the NR readout loads of
+        // the same stage are younger); then stage the next shot ----
+        QDEC_STAMP(5);
+        wait_vmem<Io::NR>();
+        Io::patch_tail(a.syn, a.B, m, shot, io.syn, io.syn_shift, lane);
+        wave_lds_sync();
+        QDEC_STAMP(0);
         int sbit[RC];
+        const uint8_t* srow = io.syn_row();
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) {
             const int i = rc * 64 + lane;
-            sbit[rc] = (i < m && a.syn) ? (a.syn[shot * m + i] & 1) : 0;
+            sbit[rc] = (i < m && a.syn) ? (int)(srow[i] & 1) : 0;
         }
-        if (a.syn_flags) {
+        wait_lds();
+        io.stage(g, a, shot + gridDim.x, buf ^ 1, lane);
+        if (!LEAN && a.syn_flags) {
             const bool use_b = (a.syn_flags & 1) && a.base;
             const bool use_r = (a.syn_flags & 2) && a.readout;
             uint64_t Xf[RV];
 #pragma unroll
             for (int w = 0; w < RV; ++w) {
-                const int q = w * 64 + lane;
+                const int q = col_of(w);
                 int v = 0;
                 if (q < g.n_data) {
                     if (use_b) v ^= a.base[shot * g.n_data + q];
@@ -112,10 +160,10 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
             }
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
-                int c = 0;
+                uint64_t acc = 0;
 #pragma unroll
-                for (int w = 0; w < RV; ++w) c += __popcll(smask[rc][w] & Xf[w]);
-                sbit[rc] ^= c & 1;
+                for (int w = 0; w < RV; ++w) acc ^= smask[rc][w] & Xf[w];
+                sbit[rc] ^= __popcll(acc) & 1;
             }
         }
 
@@ -126,18 +174,19 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
 #pragma unroll
             for (int k = 0; k < kDC; ++k) {
                 vp[rv][k] = L[rv];
-                v2c[etab[rv][k] & 0xffff] = L[rv];
+                if (!(rv < D3R && k == 3)) v2c[etab[rv][k] & 0xffff] = L[rv];
             }
-        __syncthreads();
+        wave_lds_sync();
 
+        QDEC_STAMP(1);
         T Q[RV];
         uint64_t X[RV];
         int pres[RC];
         int it = 1;
         bool conv = false;
         for (; it <= a.max_iter; ++it) {
-            const T alpha = alpha_at<T>(it, a.ms_scaling);
-            // ---- check pass: state (m1, m2 | parity) ----
+            const T alpha = alpha_bits<T>(it, a.ms_scaling);
+            // ---- check pass: state (m1, m2) with the parity in both signs ----
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
                 const int i = rc * 64 + lane;
@@ -155,43 +204,67 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                         m1 = fmin(m1, av);
                     par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign
                 }
+                // both minima carry the parity in their sign bit (they are >= +0)
                 V2 s2;
-                s2.x = m1;
-                s2.y = FBits<T>::from(FBits<T>::to(m2) | (par ? kSign : (U)0));
+                s2.x = par ? -m1 : m1;
+                s2.y = par ? -m2 : m2;
                 *reinterpret_cast<V2*>(st + 2 * i) = s2;
             }
-            __syncthreads();
+            wave_lds_sync();
 
-            // ---- variable pass ----
+            // ---- variable pass (states of round rv+1 in flight while rv computes) ----
+            V2 sn[kDC];
+#pragma unroll
+            for (int k = 0; k < kDC; ++k)
+                if (!(0 < D3R && k == 3)) sn[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[0][k] >> 16));
 #pragma unroll
             for (int rv = 0; rv < RV; ++rv) {
+                constexpr int kd4 = kDC;
+                const int KD = rv < D3R ? 3 : kd4;
+                V2 sc[kDC];
+#pragma unroll
+                for (int k = 0; k < kDC; ++k) sc[k] = sn[k];
+                if (rv + 1 < RV) {
+#pragma unroll
+                    for (int k = 0; k < kDC; ++k)
+                        if (!(rv + 1 < D3R && k == 3))
+                            sn[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[rv + 1 < RV ? rv + 1 : rv][k] >> 16));
+                }
+                // |c| = alpha * ((|v| == m1) ? m2 : m1), sign = parity ^ (v <= 0);
+                // the state's signs carry the parity, so one select picks both
                 T c[kDC];
 #pragma unroll
                 for (int k = 0; k < kDC; ++k) {
-                    const V2 s2 = *reinterpret_cast<const V2*>(st + 2 * (etab[rv][k] >> 16));
-                    const U mb = FBits<T>::to(s2.y);
-                    const T m2 = FBits<T>::from(mb & ~kSign);
-                    const T v = vp[rv][k];
-                    const T y = ((fabs(v) == s2.x) ? m2 : s2.x) * alpha;
-                    const bool neg = ((mb & kSign) != 0) ^ (v <= (T)0);
-                    c[k] = neg ? -y : y;
+                    if (k < KD) {
+                        const V2 s2 = sc[k];
+                        const T v = vp[rv][k];
+                        const T y = ((fabs(v) == fabs(s2.x)) ? s2.y : s2.x) * alpha;
+                        c[k] = (v <= (T)0) ? -y : y;
+                    }
                 }
                 T pre[kDC];
                 T acc = L[rv];
 #pragma unroll
                 for (int k = 0; k < kDC; ++k) {
-                    pre[k] = acc;
-                    acc += c[k];
+                    if (k < KD) {
+                        pre[k] = acc;
+                        acc += c[k];
+                    }
                 }
-                Q[rv] = acc;
+                if constexpr (!LEAN) Q[rv] = acc;
                 X[rv] = __ballot(acc <= (T)0);
+                // ldpc: out_k = pre_k + (sum of the later c); the last one adds an
+                // empty sum (+0), which can only turn -0 into +0: both are <= 0 and
+                // have |v| = 0, so the message is used identically either way
                 T suf = (T)0;
 #pragma unroll
                 for (int k = kDC - 1; k >= 0; --k) {
-                    const T out = pre[k] + suf;
-                    suf += c[k];
-                    vp[rv][k] = out;
-                    v2c[etab[rv][k] & 0xffff] = out;  // pads -> dummy element
+                    if (k < KD) {
+                        const T out = (k == KD - 1) ? pre[k] : pre[k] + suf;
+                        suf = (k == KD - 1) ? c[k] : suf + c[k];
+                        vp[rv][k] = out;
+                        v2c[etab[rv][k] & 0xffff] = out;  // pads -> dummy element
+                    }
                 }
             }
 
@@ -205,28 +278,37 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                 pres[rc] = (sbit[rc] ^ __popcll(acc)) & 1;
                 bad |= pres[rc];
             }
-            __syncthreads();  // v2c scatter complete before the next check pass
+            wave_lds_sync();  // v2c scatter complete before the next check pass
             if (__ballot(bad) == 0ull) {
                 conv = true;
                 break;
             }
         }
         const int iters = conv ? it : a.max_iter;
-        if (lane == 0 && a.iters) a.iters[shot] = iters;
-#pragma unroll
-        for (int rv = 0; rv < RV; ++rv) {
-            const int j = rv * 64 + lane;
-            if (j < n) xh[j] = (uint8_t)((X[rv] >> lane) & 1);
+        QDEC_STAMP(2);
+        QDEC_COUNT(8, iters);
+        QDEC_COUNT(9, 1);
+        // this shot's readout: wait before any store of this shot, so the kStaged
+        // most recent vector-memory operations are exactly the next shot's stage
+        const bool need_rd = !(DEFER && !conv) && a.readout && a.fail && g.k > 0;
+        if (need_rd) {
+            wait_vmem<Io::kStaged>();
+            Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd + 256 * Io::NR * buf, io.rd_shift[buf], lane);
         }
-        if (a.llr_out) {
+        if (lane == 0 && a.iters) a.iters[shot] = iters;
+        // hard decision by column (slot order -> xh[column])
+#pragma unroll
+        for (int rv = 0; rv < RV; ++rv) xh[col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
+        if (!LEAN && a.llr_out) {
             T* lo = reinterpret_cast<T*>(a.llr_out);
 #pragma unroll
             for (int rv = 0; rv < RV; ++rv) {
-                const int j = rv * 64 + lane;
+                const int j = col_of(rv);
                 if (j < n) lo[shot * n + j] = Q[rv];
             }
         }
-        __syncthreads();
+        wave_lds_sync();
+        QDEC_STAMP(3);
         if (DEFER && !conv) {
             int slot = 0;
             if (lane == 0) slot = atomicAdd(a.q_count, 1);
@@ -238,11 +320,33 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                 if (i < m) a.q_r[(int64_t)slot * m + i] = (uint8_t)pres[rc];
             }
             if (lane == 0) a.q_idx[slot] = shot;
+        } else if (LEAN || (g.fold_blocks == 1 && !a.corr_out)) {
+            if (!LEAN && a.x_out)
+                for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
+            int any_fail = 0;
+            if (a.fail && a.readout && g.k > 0) {
+                uint64_t Xc[RV];  // hard decision by column
+#pragma unroll
+                for (int w = 0; w < RV; ++w) Xc[w] = __ballot(xh[w * 64 + lane] & 1);
+                any_fail = fail_from_words<RV, !LEAN>(g, a, shot, lane, Xc, io.rd_row(buf), io.lz);
+            }
+            if (lane == 0) {
+                if (a.status) a.status[shot] = (uint8_t)(conv ? 3 : 0);
+                if (a.ssf_steps) a.ssf_steps[shot] = 0;
+                if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+            }
         } else {
-            finalize_shot(g, a, shot, xh, conv, conv, 0, lane);
+            finalize_shot_io(g, a, shot, xh, conv, conv, 0, lane, io.rd_row(buf), io.lz);
         }
-        __syncthreads();
+        wave_lds_sync();
+        QDEC_STAMP(4);
     }
+#ifdef QDEC_STAMPS
+    QDEC_COUNT(10, __builtin_amdgcn_s_memtime() - qdec_t0);
+    QDEC_COUNT(11, __builtin_amdgcn_s_memrealtime() - qdec_r0);
+    QDEC_COUNT(12, 1);
+#endif
+    QDEC_FLUSH();
 }
 
 }  // namespace qdec

@@ -7,6 +7,49 @@
 
 namespace qdec {
 
+// Development-only phase timers (build with -DQDEC_STAMPS: `python -m
+// exp_ldpc_amd.build --stamps`): per-wave s_memtime deltas accumulated into a
+// device array, read with qd_dev_read_stamps.
+#ifdef QDEC_STAMPS
+static __device__ unsigned long long qdec_stamps[64];
+#define QDEC_STAMP_DECL                                                   \
+    unsigned long long qdec_acc_[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+    unsigned long long qdec_st_prev_ = __builtin_amdgcn_s_memtime();
+#define QDEC_STAMP(k)                                                  \
+    do {                                                               \
+        const unsigned long long qdec_n_ = __builtin_amdgcn_s_memtime(); \
+        qdec_acc_[k] += qdec_n_ - qdec_st_prev_;                       \
+        qdec_st_prev_ = qdec_n_;                                       \
+    } while (0)
+#define QDEC_COUNT(k, v) qdec_acc_[k] += (unsigned long long)(v)
+#define QDEC_FLUSH()                                                          \
+    do {                                                                      \
+        if ((threadIdx.x & 63) == 0)                                          \
+            for (int qdec_k_ = 0; qdec_k_ < 16; ++qdec_k_) atomicAdd(&qdec_stamps[qdec_k_], qdec_acc_[qdec_k_]); \
+    } while (0)
+#else
+#define QDEC_STAMP_DECL
+#define QDEC_STAMP(k) \
+    do {              \
+    } while (0)
+#define QDEC_COUNT(k, v) \
+    do {                 \
+    } while (0)
+#define QDEC_FLUSH() \
+    do {             \
+    } while (0)
+#endif
+
+// Orders this wave's LDS accesses across lanes.  A wave's LDS operations
+// execute in issue order, so for a one-wave workgroup (or a wave working on its
+// own LDS region) it is enough to keep the compiler from moving them; unlike
+// __syncthreads() this does not wait for outstanding LDS operations to drain.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <typename T>
 struct Big;
 template <>
@@ -209,6 +252,194 @@ __device__ inline void finalize_shot(const DevGraph& g, const DecodeArgs& a, int
         if (a.ssf_steps) a.ssf_steps[shot] = steps;
         if (a.fail) a.fail[shot] = (uint8_t)any_fail;
     }
+}
+
+// ---------------------------------------------------------------- shot I/O staging
+// Per-wave LDS staging of shot inputs with LDS-DMA loads (global_load_lds: no
+// VGPR destination, completes while the wave decodes).  At the start of shot s
+// the wave stages the syndrome row and the readout row of shot s+1 (one
+// persistent-loop step ahead), so no HBM round trip sits on a shot's critical
+// path.  Rows are fetched as whole dwords (64 lanes x 4 B per instruction) from
+// the dword-aligned address at or below the row start; `shift` is the row's
+// byte offset inside the staged bytes.  The readout is double buffered (shot s
+// reads its buffer at the end while s+1's lands).  Every stage issues the same
+// number of loads (past the batch end it re-reads shot 0; lanes past the buffer
+// read its last whole dword), so consumers wait with a counted vmcnt: vector
+// memory operations retire in issue order and the kStaged most recent ones are
+// the next shot's.  The final 1-3 bytes of a buffer whose length is not a
+// multiple of 4 are not covered by a whole dword; the shot that needs them
+// patches them in with byte loads (patch_tail).
+constexpr int kLzLdsBytes = 2048;
+
+__host__ __device__ inline bool lz_in_lds(const DevGraph& g) {
+    return g.k > 0 && (size_t)g.k * g.lz_words * 8 <= (size_t)kLzLdsBytes;
+}
+
+template <int RC, int NW>
+struct ShotIo {
+    static constexpr int NS = (64 * RC + 3 + 255) / 256;  // syndrome glds per stage
+    static constexpr int NR = (64 * NW + 3 + 255) / 256;  // readout glds per stage
+    static constexpr int kStaged = NS + NR;
+    __host__ __device__ static size_t bytes(const DevGraph& g) {
+        size_t b = 256 * (size_t)(NS + 2 * NR);
+        if (lz_in_lds(g)) b += ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16;
+        return b;
+    }
+    uint8_t* syn;        // [NS*256]     staged syndrome row of the next shot
+    uint8_t* rd;         // [2][NR*256]  staged readout rows, by loop parity
+    const uint64_t* lz;  // LDS copy or the global table
+    int syn_shift;       // byte offset of the staged syndrome row
+    int rd_shift[2];
+
+    __device__ ShotIo(const DevGraph& g, unsigned char* base) {
+        syn = base;
+        rd = base + 256 * NS;
+        uint64_t* l = reinterpret_cast<uint64_t*>(base + 256 * (NS + 2 * NR));
+        lz = lz_in_lds(g) ? l : g.lz;
+        syn_shift = 0;
+        rd_shift[0] = rd_shift[1] = 0;
+    }
+    __device__ void init(const DevGraph& g, int lane) {
+        if (lz_in_lds(g)) {
+            uint64_t* l = const_cast<uint64_t*>(lz);
+            for (int e = lane; e < g.k * g.lz_words; e += 64) l[e] = g.lz[e];
+        }
+    }
+    // N glds of whole dwords covering row `row` of a [B][len] byte buffer into
+    // dst: a uniform base address plus 32-bit lane offsets, clamped to the
+    // buffer's last whole dword.
+    template <int N>
+    __device__ static int stage_row(const uint8_t* buf, int64_t B, int len, int64_t row, uint8_t* dst, int lane,
+                                    const uint8_t* dummy) {
+        const int64_t total_dw = B * (int64_t)len / 4;  // whole dwords inside the buffer
+        if (!buf || len <= 0 || total_dw <= 0) {
+#pragma unroll
+            for (int c = 0; c < N; ++c) __builtin_amdgcn_global_load_lds(dummy, dst + 256 * c, 4, 0, 0);
+            return 0;
+        }
+        const int64_t start = row * len;
+        const int64_t dw0 = start >> 2;
+        const uint8_t* base = buf + 4 * dw0;
+        const int64_t lim64 = total_dw - 1 - dw0;  // last loadable dword, relative (>= 0)
+        const int lim = lim64 > 0x3fffffff ? 0x3fffffff : (int)lim64;
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const int rel = min(64 * c + lane, lim);
+            __builtin_amdgcn_global_load_lds(base + 4 * rel, dst + 256 * c, 4, 0, 0);
+        }
+        return (int)(start & 3);
+    }
+    // exactly kStaged LDS-DMA loads: syndrome and readout rows of `shot` (shot 0 past B)
+    __device__ void stage(const DevGraph& g, const DecodeArgs& a, int64_t shot, int buf, int lane) {
+        if (shot >= a.B) shot = 0;
+        const uint8_t* dummy = reinterpret_cast<const uint8_t*>(g.col_idx);
+        syn_shift = stage_row<NS>(a.syn, a.B, g.m, shot, syn, lane, dummy);
+        rd_shift[buf] = stage_row<NR>(a.readout, a.B, g.n_data, shot, rd + 256 * NR * buf, lane, dummy);
+    }
+    // bytes [total_dw*4, B*len) of the last row (only when B*len % 4 != 0), after the row's wait
+    __device__ static void patch_tail(const uint8_t* buf, int64_t B, int len, int64_t row, uint8_t* dst, int shift,
+                                      int lane) {
+        if (!buf || len <= 0 || row != B - 1) return;
+        const int64_t total = B * (int64_t)len, covered = total / 4 * 4;
+        const int64_t start = row * len;
+        const int64_t q = covered + lane;
+        if (q < total && q >= start) dst[shift + (q - start)] = buf[q];
+    }
+    __device__ uint8_t* syn_row() const { return syn + syn_shift; }
+    __device__ const uint8_t* rd_row(int buf) const { return rd + 256 * NR * buf + rd_shift[buf]; }
+};
+
+// Waits until at most N of this wave's vector-memory operations (LDS-DMA loads
+// included) are outstanding, and orders that before the following LDS reads.
+template <int N>
+__device__ __forceinline__ void wait_vmem() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    wave_lds_sync();
+}
+// Waits for this wave's LDS reads to return (before an LDS-DMA overwrites them).
+__device__ __forceinline__ void wait_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// finalize_shot with the readout taken from the LDS staging buffer `rdl`
+// (columns w*64 + lane) and the logicals from `lzs` (LDS or global).
+__device__ inline void finalize_shot_io(const DevGraph& g, const DecodeArgs& a, int64_t shot, const uint8_t* xh,
+                                        bool conv, bool satisfied, int steps, int lane, const uint8_t* rdl,
+                                        const uint64_t* lzs) {
+    const int n = g.n;
+    if (a.x_out)
+        for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    int lpar[kMaxLogicalRounds] = {0, 0, 0, 0};
+    if (a.corr_out || want_fail) {
+        for (int w0 = 0; w0 < g.lz_words; ++w0) {
+            const int q = w0 * 64 + lane;
+            int cb = 0;
+            if (q < g.n_data) {
+                cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
+                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+                if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+            }
+            if (want_fail) {
+                const int v = (q < g.n_data) ? ((rdl[q] ^ cb) & 1) : 0;
+                const unsigned long long word = __ballot(v);
+#pragma unroll
+                for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                    const int r = rr * 64 + lane;
+                    if (r < g.k) lpar[rr] ^= __popcll(lzs[(size_t)r * g.lz_words + w0] & word) & 1;
+                }
+            }
+        }
+    }
+    int any_fail = 0;
+    if (want_fail) {
+        int f = 0;
+#pragma unroll
+        for (int rr = 0; rr < kMaxLogicalRounds; ++rr) f |= lpar[rr];
+        any_fail = __ballot(f) != 0ull;
+    }
+    if (lane == 0) {
+        if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
+        if (a.ssf_steps) a.ssf_steps[shot] = steps;
+        if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+    }
+}
+
+// Fused failure check from the hard decision held as ballot words
+// (X[w] bit l = column 64 w + l), for graphs without a spacetime fold:
+// corr = base ^ x, fail = any_r parity(lz_r . (readout ^ corr)).  Readout from
+// the LDS staging area, logicals from `lzs`.
+template <int NW, bool WITH_BASE>
+__device__ inline int fail_from_words(const DevGraph& g, const DecodeArgs& a, int64_t shot, int lane,
+                                      const uint64_t (&X)[NW], const uint8_t* rdl, const uint64_t* lzs) {
+    uint64_t R[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        R[w] = 0;
+        if (w < g.lz_words) {
+            const int q = w * 64 + lane;
+            int v = 0;
+            if (q < g.n_data) {
+                v = (int)rdl[q];
+                if (WITH_BASE && a.base) v ^= a.base[shot * g.n_data + q];
+            }
+            R[w] = __ballot(v & 1) ^ X[w];  // columns >= n_data: lz bits are zero
+        }
+    }
+    int f = 0;
+#pragma unroll
+    for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+        const int r = rr * 64 + lane;
+        if (r < g.k) {
+            int p = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (w < g.lz_words) p += __popcll(lzs[(size_t)r * g.lz_words + w] & R[w]);
+            f |= p & 1;
+        }
+    }
+    return __ballot(f) != 0ull;
 }
 
 }  // namespace qdec

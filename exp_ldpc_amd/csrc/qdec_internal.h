@@ -61,13 +61,17 @@ struct DevGraph {
     const int32_t* col_idx;
     const int32_t* col_ptr;       // [n+1]
     const int32_t* col_edge;      // [E] CSR edge ids of column j, ascending row
-    // min-sum wave kernel with compressed check state (qdec_bp_ms.h): variable
-    // edge k scatters its v2c message to element (etab & 0xffff) and gathers
-    // check state (etab >> 16); pads -> a dummy element / the zero state m_pad.
+    // min-sum wave kernel with compressed check state (qdec_bp_ms.h).  Variables
+    // sit in lane slots sorted by degree (ms_vslot); slot edge k scatters its v2c
+    // message to element (etab & 0xffff) and gathers check state (etab >> 16);
+    // pads -> a dummy element / the zero state m_pad.
     // Row positions inside a check's v2c row are chosen on the host so the
     // scatter has at most 2-way bank conflicts (ms_layout in qdec_abi.cpp).
     const uint32_t* ms_etab[2];   // [kDC][n_pad], per precision (element strides differ)
-    const uint64_t* ms_smask;     // [n_pad/64][m_pad] columns of check i inside 64-column word w
+    const uint64_t* ms_smask;     // [n_pad/64][m_pad] slots of check i's columns inside 64-slot word w
+    const uint16_t* ms_vslot;     // [n_pad] column held by lane slot s (pads: n_pad + s % 64)
+    const void* ms_prior[2];      // [precision][n_pad] min-sum priors in slot order
+    int ms_d3r;                   // leading 64-slot rounds whose variables all have degree <= 3
     // flip sets (SSF)
     int n_gen, g_pad, g_wmax;
     const uint8_t* g_w;           // [g_pad]

@@ -1,0 +1,39 @@
+"""Dev: phase timers of the min-sum kernel (needs libqdec_hip_stamps.so)."""
+import ctypes as C, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["QDEC_LIB"] = os.path.join(ROOT, "exp_ldpc_amd", "libqdec_hip_stamps.so")
+sys.path.insert(0, ROOT)
+import numpy as np, torch
+from exp_ldpc_amd import _abi
+from exp_ldpc_amd.decoder import Decoder
+import bench
+lib = _abi.load()
+lib.qd_dev_read_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
+code = bench.load_code()
+hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
+B = 1 << 18
+dev = torch.device("cuda", 0)
+names = ["wait_syn", "stage+init", "iterations", "post", "finalize", "loop_top"]
+for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
+    dec = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, flip_sets=hx, logicals=lz)
+    syn = torch.empty((B, 108), dtype=torch.uint8, device=dev)
+    rd = torch.empty((B, 225), dtype=torch.uint8, device=dev)
+    dec.sample_storage_device(0, p, p, 1, 0, 0, B, syn, rd)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    status = torch.empty(B, dtype=torch.uint8, device=dev)
+    fail = torch.empty(B, dtype=torch.uint8, device=dev)
+    for label, kw in (("full", dict(syn=syn, readout=rd, iters=iters, status=status, fail=fail)),
+                      ("no_fail", dict(syn=syn, iters=iters, status=status))):
+        for ssf in (True, False):
+            dec.decode_device(B, ssf=ssf, **kw)
+            torch.cuda.synchronize()
+            buf = np.zeros(64, np.uint64)
+            lib.qd_dev_read_stamps(buf.ctypes.data, 64, 1)
+            dec.decode_device(B, ssf=ssf, **kw)
+            torch.cuda.synchronize()
+            lib.qd_dev_read_stamps(buf.ctypes.data, 64, 1)
+            shots = int(buf[9]); its = int(buf[8])
+            print(f"p={p} {label} ssf={int(ssf)} shots={shots} iters/shot={its/shots:.2f} cycles/shot: " +
+                  " ".join(f"{n}={buf[i]/shots:.0f}" for i, n in enumerate(names)) +
+                  f" | per-iter={buf[2]/its:.0f} | waves={int(buf[12])} ticks/wave={buf[10]/max(1,buf[12]):.0f}"
+                  f" real_us/wave={buf[11]/max(1,buf[12])/100:.1f}", flush=True)
