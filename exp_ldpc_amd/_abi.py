@@ -19,7 +19,7 @@ except Exception:  # pragma: no cover - torch is optional for the ABI itself
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("QDEC_LIB", os.path.join(HERE, "libqdec_hip.so"))
+LIB_PATH = os.environ.get("QDEC_LIB") or os.path.join(HERE, "libqdec_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "qdec.h")
 
 QD_PRODUCT_SUM, QD_MIN_SUM = 0, 1

@@ -356,7 +356,11 @@ void attach_queue(qd_graph* G, DecodeArgs& a) {
         if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
         G->qws = nullptr;
         G->q_cap = 0;
-        const size_t bytes = 256 + (size_t)a.B * (8 + (size_t)g.n + (size_t)g.m) + 256;
+        // byte format: idx[B] | x[B][n] | r[B][m]; packed format (wave kernels) reuses
+        // the x region for [B][1 + 2 n_pad/64 + m_pad/64] u64 entries
+        const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
+        const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
+        const size_t bytes = 256 + (size_t)a.B * (8 + xr) + 256;
         hip_check(hipMalloc(&G->qws, bytes), "hipMalloc queue");
         G->q_cap = a.B;
     }
@@ -365,6 +369,7 @@ void attach_queue(qd_graph* G, DecodeArgs& a) {
     a.q_idx = reinterpret_cast<int64_t*>(base + 256);
     a.q_x = base + 256 + (size_t)G->q_cap * 8;
     a.q_r = a.q_x + (size_t)G->q_cap * g.n;
+    a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
 }
 
 void* message_scratch(qd_graph* G, int precision, size_t* bytes) {

@@ -257,16 +257,30 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
         }
         if (DEFER && !conv) {
             // hand the shot to the SSF kernel: hard decision + residual syndrome
-            int slot = 0;
-            if (lane == 0) slot = atomicAdd(a.q_count, 1);
-            slot = __shfl(slot, 0);
-            for (int j = lane; j < n; j += 64) a.q_x[(int64_t)slot * n + j] = xh[j];
+            if (a.q_packed) {
+                uint64_t xw[RV], rw[RC], dw[RV];
+                const bool with_rd = a.readout && a.fail && g.k > 0;
 #pragma unroll
-            for (int rc = 0; rc < RC; ++rc) {
-                const int i = rc * 64 + lane;
-                if (i < m) a.q_r[(int64_t)slot * m + i] = (uint8_t)pres[rc];
+                for (int w = 0; w < RV; ++w) {
+                    const int q = w * 64 + lane;
+                    xw[w] = __ballot(q < n && (xh[q] & 1));
+                    dw[w] = with_rd ? __ballot(q < g.n_data && (a.readout[shot * g.n_data + q] & 1)) : 0ull;
+                }
+#pragma unroll
+                for (int rc = 0; rc < RC; ++rc) rw[rc] = __ballot(pres[rc]);
+                queue_push_packed<RV, RC>(a, shot, xw, rw, dw, lane);
+            } else {
+                int slot = 0;
+                if (lane == 0) slot = atomicAdd(a.q_count, 1);
+                slot = __shfl(slot, 0);
+                for (int j = lane; j < n; j += 64) a.q_x[(int64_t)slot * n + j] = xh[j];
+#pragma unroll
+                for (int rc = 0; rc < RC; ++rc) {
+                    const int i = rc * 64 + lane;
+                    if (i < m) a.q_r[(int64_t)slot * m + i] = (uint8_t)pres[rc];
+                }
+                if (lane == 0) a.q_idx[slot] = shot;
             }
-            if (lane == 0) a.q_idx[slot] = shot;
         } else {
             finalize_shot(g, a, shot, xh, conv, conv, 0, lane);
         }
@@ -294,15 +308,24 @@ constexpr int kSsfWaves = 4;
 template <int RG>
 struct SsfLds {
     static constexpr int GP = 64 * RG;
-    __host__ __device__ static size_t shared_bytes() { return (size_t)GP * 4 * (kGenW + kGenLC / 4 + kGenW / 2); }
+    static constexpr int kStage = 3;  // packed queue entries staged per wave (two slots ahead)
+    __host__ __device__ static size_t table_bytes() { return (size_t)GP * 4 * (kGenW + kGenLC / 4 + kGenW / 2); }
+    __host__ __device__ static size_t shared_bytes(const DevGraph& g) {
+        return table_bytes() + (lz_in_lds(g) ? ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16 : 0);
+    }
     __host__ __device__ static size_t wave_bytes(const DevGraph& g) {
-        return (((size_t)g.m_pad + 64) * 4 + (size_t)GP * 4 * 2 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16;
+        return (((size_t)g.m_pad + 64) * 4 + (size_t)GP * 4 * 2 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16 +
+               256 * kStage;
     }
 };
 
-template <int RG>
+// XW/RW: words of the packed queue entries (hard decision by column, residual
+// by check) written by the wave BP kernels (queue_push_packed).
+template <int RG, int XW, int RW>
 __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
     constexpr int GP = SsfLds<RG>::GP;
+    constexpr int QW = QEntry<XW, RW>::QW;
+    static_assert(2 * QW <= 64, "entry staging");
     constexpr int NLW = kGenLC / 4;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // shared: qubit local-check masks, packed u8 local-check ids, packed u16 qubit ids
@@ -310,12 +333,15 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
     uint32_t* lct = qmt + kGenW * GP;                   // [NLW][GP]   (pad id m_pad -> zero residual)
     uint32_t* qt = lct + NLW * GP;                      // [kGenW/2][GP]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    unsigned char* wbase = smem + SsfLds<RG>::shared_bytes() + (size_t)wave * SsfLds<RG>::wave_bytes(g);
+    uint64_t* lzs_lds = reinterpret_cast<uint64_t*>(smem + SsfLds<RG>::table_bytes());
+    const uint64_t* lzs = lz_in_lds(g) ? lzs_lds : g.lz;
+    unsigned char* wbase = smem + SsfLds<RG>::shared_bytes(g) + (size_t)wave * SsfLds<RG>::wave_bytes(g);
     uint32_t* sres = reinterpret_cast<uint32_t*>(wbase);      // [m_pad + 64] residual (pads stay 0)
     int* key = reinterpret_cast<int*>(sres + g.m_pad + 64);   // [GP] cached best keys
     uint32_t* slt = reinterpret_cast<uint32_t*>(key + GP);    // [GP] local syndromes of listed gens
     uint8_t* list = reinterpret_cast<uint8_t*>(slt + GP);     // [GP] listed generators
     uint8_t* xh = list + GP;                                  // [n_pad + 64]
+    uint8_t* ent = wbase + SsfLds<RG>::wave_bytes(g) - 256 * SsfLds<RG>::kStage;  // [kStage][256] queue entries
     const int m = g.m, n = g.n;
 
     for (int e = threadIdx.x; e < GP; e += 64 * kSsfWaves) {
@@ -327,23 +353,58 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
         for (int k = 0; k < kGenW / 2; ++k)
             qt[k * GP + e] = (uint32_t)g.g_q[(2 * k) * g.g_pad + e] | ((uint32_t)g.g_q[(2 * k + 1) * g.g_pad + e] << 16);
     }
+    if (lz_in_lds(g))
+        for (int e = threadIdx.x; e < g.k * g.lz_words; e += 64 * kSsfWaves) lzs_lds[e] = g.lz[e];
     for (int e = lane; e < g.m_pad + 64; e += 64) sres[e] = 0;
     for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
     __syncthreads();
 
     const int count = *a.q_count;
+    // entry of queue slot `sl` into staging buffer `b` (one LDS-DMA load; past
+    // the queue end it re-reads entry 0, so every stage issues exactly one)
+    auto stage_entry = [&](int sl, int b) {
+        const int64_t e = sl < count ? sl : 0;
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(a.q_w + e * QW) + 4 * min(lane, 2 * QW - 1);
+        __builtin_amdgcn_global_load_lds(src, ent + 256 * b, 4, 0, 0);
+    };
+    const int stride = gridDim.x * kSsfWaves;
+    const bool lean_fin = !a.x_out && !a.corr_out && !a.base && g.fold_blocks == 1;
+    const bool want_fail = a.fail && a.readout && g.k > 0;
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
     const int nlcw = (g.g_nlcmax + 3) / 4;
-    for (int slot = blockIdx.x * kSsfWaves + wave; slot < count; slot += gridDim.x * kSsfWaves) {
-        const int64_t shot = a.q_idx[slot];
-        for (int j = lane; j < n; j += 64) xh[j] = a.q_x[(int64_t)slot * n + j];
-        int w_local = 0;
-        for (int i = lane; i < m; i += 64) {
-            const uint32_t r = a.q_r[(int64_t)slot * m + i];
-            sres[i] = r;
-            w_local += (int)r;
+    QDEC_STAMP_DECL
+    const int slot0 = blockIdx.x * kSsfWaves + wave;
+    stage_entry(slot0, 0);
+    stage_entry(slot0 + stride, 1);
+    int sb = 0;
+    for (int slot = slot0; slot < count; slot += stride, sb = sb == 2 ? 0 : sb + 1) {
+        QDEC_STAMP(12);
+        // entry staged two slots ahead; the next slot's stage is younger
+        wait_vmem<1>();
+        const uint64_t* ew = reinterpret_cast<const uint64_t*>(ent + 256 * sb);
+        const int64_t shot = (int64_t)ew[0];
+        uint64_t X[XW], R[RW], D[XW];
+#pragma unroll
+        for (int w = 0; w < XW; ++w) {
+            X[w] = ew[1 + w];
+            D[w] = ew[1 + XW + RW + w];
         }
-        int sw = wave_sum_i32(w_local);
+#pragma unroll
+        for (int w = 0; w < RW; ++w) R[w] = ew[1 + XW + w];
+        wait_lds();
+        stage_entry(slot + 2 * stride, sb == 0 ? 2 : sb - 1);
+#pragma unroll
+        for (int w = 0; w < XW; ++w) {
+            const int j = w * 64 + lane;
+            xh[j] = j < n ? (uint8_t)((X[w] >> lane) & 1) : (uint8_t)0;
+        }
+        int sw = 0;
+#pragma unroll
+        for (int w = 0; w < RW; ++w) {
+            const int i = w * 64 + lane;
+            sres[i] = i < m ? (uint32_t)((R[w] >> lane) & 1) : 0u;
+            sw += __popcll(R[w]);
+        }
         wave_lds_sync();
         uint32_t slo[RG];
         int steps = 0;
@@ -378,6 +439,8 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
             }
             first = false;
             wave_lds_sync();
+            QDEC_STAMP(0);
+            QDEC_COUNT(5, nl);
             // ---- 2. score the listed generators ----
             for (int c0 = 0; c0 < nl; c0 += 64) {
                 const int idx = c0 + lane;
@@ -392,6 +455,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
                 }
             }
             wave_lds_sync();
+            QDEC_STAMP(1);
             // ---- 3. pick (score, -g), then the lowest subset reaching the score ----
             int kv = INT_MIN;
 #pragma unroll
@@ -426,6 +490,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
                 }
             }
             if (tsel < 0) break;  // unreachable: the best score is some subset's score
+            QDEC_STAMP(2);
             // ---- 4. apply the flip ----
             const uint32_t fm = (uint32_t)wave_xor_masked(lane < kGenW && ((tsel >> lane) & 1) ? qk : 0u);
             const int gain = score * __builtin_popcount(tsel) / kSsfScale;
@@ -440,10 +505,43 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
             wave_lds_sync();
             sw -= gain;
             ++steps;
+            QDEC_STAMP(3);
+            QDEC_COUNT(6, 1);
         }
-        finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
+        QDEC_STAMP(13);
+        if (lean_fin) {
+            int any_fail = 0;
+            if (want_fail) {  // readout words came with the queue entry
+                uint64_t Rd[XW];
+#pragma unroll
+                for (int w = 0; w < XW; ++w) Rd[w] = __ballot(xh[w * 64 + lane] & 1) ^ D[w];
+                int f = 0;
+#pragma unroll
+                for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                    const int r = rr * 64 + lane;
+                    if (r < g.k) {
+                        int par = 0;
+#pragma unroll
+                        for (int w = 0; w < XW; ++w)
+                            if (w < g.lz_words) par += __popcll(lzs[(size_t)r * g.lz_words + w] & Rd[w]);
+                        f |= par & 1;
+                    }
+                }
+                any_fail = __ballot(f) != 0ull;
+            }
+            if (lane == 0) {
+                if (a.status) a.status[shot] = (uint8_t)(sw == 0 ? 2 : 0);
+                if (a.ssf_steps) a.ssf_steps[shot] = steps;
+                if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+            }
+        } else {
+            finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
+        }
+        QDEC_STAMP(14);
+        QDEC_COUNT(7, 1);
         wave_lds_sync();
     }
+    QDEC_FLUSH_AT(16);
 }
 
 // ---------------------------------------------------------------- launcher
@@ -455,18 +553,19 @@ static size_t wave_lds_bytes(const DevGraph& g) {
            (size_t)g.n_pad + 64;
 }
 
-template <int RG>
+template <int RG, int XW, int RW>
 static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
-    const size_t lds = SsfLds<RG>::shared_bytes() + kSsfWaves * SsfLds<RG>::wave_bytes(g);
+    const size_t lds = SsfLds<RG>::shared_bytes(g) + kSsfWaves * SsfLds<RG>::wave_bytes(g);
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ssf_wave_kernel<RG>, 64 * kSsfWaves, lds);
+    hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ssf_wave_kernel<RG, XW, RW>, 64 * kSsfWaves, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
     long long grid = (long long)num_cus * per_cu;
     const long long need = (a.B + kSsfWaves - 1) / kSsfWaves;  // queue length <= B
     if (grid > need) grid = need;
     if (grid <= 0) return 0;
-    hipLaunchKernelGGL(ssf_wave_kernel<RG>, dim3((unsigned)grid), dim3(64 * kSsfWaves), lds, stream, g, a);
+    hipLaunchKernelGGL((ssf_wave_kernel<RG, XW, RW>), dim3((unsigned)grid), dim3(64 * kSsfWaves), lds, stream, g, a);
     return (int)hipGetLastError();
 }
 
@@ -490,7 +589,8 @@ template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
 static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if constexpr (METHOD == 1) {
         const size_t lds = MsLds<T>::template bytes<RC, RV>(g);
-        const bool lean = !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1;
+        const bool lean = !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1 &&
+                          (!DEFER || a.q_packed);
         // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
             if (g.ms_d3r >= 2) {
@@ -511,7 +611,12 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
 }
 
 template <typename T, int METHOD, int RC, int RV, int DRC>
-static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hipStream_t stream) {
+    DecodeArgs a = a0;
+    // the wave SSF kernel reads the packed queue (register-owned generators, u8 local-check ids)
+    const bool ssf_wave = g.n_gen <= 128 && g.g_lc8;
+    a.q_packed = a.ssf && ssf_wave ? 1 : 0;
+    a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
     if (!a.ssf) {
         record_ev(a, 0, stream);
         const int rc = launch_bp_wave<T, METHOD, RC, RV, DRC, false>(g, a, num_cus, stream);
@@ -526,8 +631,9 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipS
     int rc = launch_bp_wave<T, METHOD, RC, RV, DRC, true>(g, a, num_cus, stream);
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
-    if (g.n_gen <= 128 && g.g_lc8) {  // register-owned generators, u8 local-check ids
-        rc = g.n_gen <= 64 ? launch_ssf_wave<1>(g, a, num_cus, stream) : launch_ssf_wave<2>(g, a, num_cus, stream);
+    if (ssf_wave) {
+        rc = g.n_gen <= 64 ? launch_ssf_wave<1, RV, RC>(g, a, num_cus, stream)
+                           : launch_ssf_wave<2, RV, RC>(g, a, num_cus, stream);
         record_ev(a, 2, stream);
         return rc;
     }

@@ -290,10 +290,10 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
         QDEC_COUNT(9, 1);
         // this shot's readout: wait before any store of this shot, so the kStaged
         // most recent vector-memory operations are exactly the next shot's stage
-        const bool need_rd = !(DEFER && !conv) && a.readout && a.fail && g.k > 0;
+        const bool need_rd = a.readout && a.fail && g.k > 0;  // the SSF queue carries it too
         if (need_rd) {
             wait_vmem<Io::kStaged>();
-            Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd + 256 * Io::NR * buf, io.rd_shift[buf], lane);
+            Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd_area(buf), io.rd_shift(buf), lane);
         }
         if (lane == 0 && a.iters) a.iters[shot] = iters;
         // hard decision by column (slot order -> xh[column])
@@ -310,16 +310,30 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
         wave_lds_sync();
         QDEC_STAMP(3);
         if (DEFER && !conv) {
-            int slot = 0;
-            if (lane == 0) slot = atomicAdd(a.q_count, 1);
-            slot = __shfl(slot, 0);
-            for (int j = lane; j < n; j += 64) a.q_x[(int64_t)slot * n + j] = xh[j];
+            if (LEAN || a.q_packed) {  // LEAN launches always use the packed queue
+                uint64_t xw[RV], rw[RC], dw[RV];
+                const uint8_t* rrow = io.rd_row(buf);
 #pragma unroll
-            for (int rc = 0; rc < RC; ++rc) {
-                const int i = rc * 64 + lane;
-                if (i < m) a.q_r[(int64_t)slot * m + i] = (uint8_t)pres[rc];
+                for (int w = 0; w < RV; ++w) {
+                    const int q = w * 64 + lane;
+                    xw[w] = __ballot(xh[q] & 1);
+                    dw[w] = need_rd ? __ballot(q < g.n_data && (rrow[q] & 1)) : 0ull;
+                }
+#pragma unroll
+                for (int rc = 0; rc < RC; ++rc) rw[rc] = __ballot(pres[rc]);
+                queue_push_packed<RV, RC>(a, shot, xw, rw, dw, lane);
+            } else {
+                int slot = 0;
+                if (lane == 0) slot = atomicAdd(a.q_count, 1);
+                slot = __shfl(slot, 0);
+                for (int j = lane; j < n; j += 64) a.q_x[(int64_t)slot * n + j] = xh[j];
+#pragma unroll
+                for (int rc = 0; rc < RC; ++rc) {
+                    const int i = rc * 64 + lane;
+                    if (i < m) a.q_r[(int64_t)slot * m + i] = (uint8_t)pres[rc];
+                }
+                if (lane == 0) a.q_idx[slot] = shot;
             }
-            if (lane == 0) a.q_idx[slot] = shot;
         } else if (LEAN || (g.fold_blocks == 1 && !a.corr_out)) {
             if (!LEAN && a.x_out)
                 for (int j = lane; j < n; j += 64) a.x_out[shot * n + j] = xh[j];
@@ -346,7 +360,7 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
     QDEC_COUNT(11, __builtin_amdgcn_s_memrealtime() - qdec_r0);
     QDEC_COUNT(12, 1);
 #endif
-    QDEC_FLUSH();
+    QDEC_FLUSH_AT(0);
 }
 
 }  // namespace qdec

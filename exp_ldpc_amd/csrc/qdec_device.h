@@ -22,10 +22,10 @@ static __device__ unsigned long long qdec_stamps[64];
         qdec_st_prev_ = qdec_n_;                                       \
     } while (0)
 #define QDEC_COUNT(k, v) qdec_acc_[k] += (unsigned long long)(v)
-#define QDEC_FLUSH()                                                          \
+#define QDEC_FLUSH_AT(off)                                                    \
     do {                                                                      \
         if ((threadIdx.x & 63) == 0)                                          \
-            for (int qdec_k_ = 0; qdec_k_ < 16; ++qdec_k_) atomicAdd(&qdec_stamps[qdec_k_], qdec_acc_[qdec_k_]); \
+            for (int qdec_k_ = 0; qdec_k_ < 16; ++qdec_k_) atomicAdd(&qdec_stamps[(off) + qdec_k_], qdec_acc_[qdec_k_]); \
     } while (0)
 #else
 #define QDEC_STAMP_DECL
@@ -35,8 +35,8 @@ static __device__ unsigned long long qdec_stamps[64];
 #define QDEC_COUNT(k, v) \
     do {                 \
     } while (0)
-#define QDEC_FLUSH() \
-    do {             \
+#define QDEC_FLUSH_AT(off) \
+    do {                   \
     } while (0)
 #endif
 
@@ -289,7 +289,7 @@ struct ShotIo {
     uint8_t* rd;         // [2][NR*256]  staged readout rows, by loop parity
     const uint64_t* lz;  // LDS copy or the global table
     int syn_shift;       // byte offset of the staged syndrome row
-    int rd_shift[2];
+    int rd_shift0, rd_shift1;  // ... of the staged readout rows (no dynamic register indexing)
 
     __device__ ShotIo(const DevGraph& g, unsigned char* base) {
         syn = base;
@@ -297,7 +297,7 @@ struct ShotIo {
         uint64_t* l = reinterpret_cast<uint64_t*>(base + 256 * (NS + 2 * NR));
         lz = lz_in_lds(g) ? l : g.lz;
         syn_shift = 0;
-        rd_shift[0] = rd_shift[1] = 0;
+        rd_shift0 = rd_shift1 = 0;
     }
     __device__ void init(const DevGraph& g, int lane) {
         if (lz_in_lds(g)) {
@@ -334,7 +334,9 @@ struct ShotIo {
         if (shot >= a.B) shot = 0;
         const uint8_t* dummy = reinterpret_cast<const uint8_t*>(g.col_idx);
         syn_shift = stage_row<NS>(a.syn, a.B, g.m, shot, syn, lane, dummy);
-        rd_shift[buf] = stage_row<NR>(a.readout, a.B, g.n_data, shot, rd + 256 * NR * buf, lane, dummy);
+        const int sh = stage_row<NR>(a.readout, a.B, g.n_data, shot, rd + 256 * NR * buf, lane, dummy);
+        if (buf) rd_shift1 = sh;
+        else rd_shift0 = sh;
     }
     // bytes [total_dw*4, B*len) of the last row (only when B*len % 4 != 0), after the row's wait
     __device__ static void patch_tail(const uint8_t* buf, int64_t B, int len, int64_t row, uint8_t* dst, int shift,
@@ -346,7 +348,9 @@ struct ShotIo {
         if (q < total && q >= start) dst[shift + (q - start)] = buf[q];
     }
     __device__ uint8_t* syn_row() const { return syn + syn_shift; }
-    __device__ const uint8_t* rd_row(int buf) const { return rd + 256 * NR * buf + rd_shift[buf]; }
+    __device__ int rd_shift(int buf) const { return buf ? rd_shift1 : rd_shift0; }
+    __device__ uint8_t* rd_area(int buf) const { return rd + 256 * NR * buf; }
+    __device__ const uint8_t* rd_row(int buf) const { return rd_area(buf) + rd_shift(buf); }
 };
 
 // Waits until at most N of this wave's vector-memory operations (LDS-DMA loads
@@ -440,6 +444,41 @@ __device__ inline int fail_from_words(const DevGraph& g, const DecodeArgs& a, in
         }
     }
     return __ballot(f) != 0ull;
+}
+
+// ---------------------------------------------------------------- packed SSF queue
+// Entry of one non-converged shot (u64 words): shot index, hard decision by
+// column (XW words), residual syndrome by check (RW words), readout by column
+// (XW words; zero when there is no fused failure check), so the SSF kernel
+// never touches the shot's rows in HBM.  Lanes 0..QW-1 store one word each.
+template <int XW, int RW>
+struct QEntry {
+    static constexpr int QW = 1 + 2 * XW + RW;
+    static_assert(QW <= 32, "queue entry");
+};
+
+template <int XW, int RW>
+__device__ inline void queue_push_packed(const DecodeArgs& a, int64_t shot, const uint64_t (&xw)[XW],
+                                         const uint64_t (&rw)[RW], const uint64_t (&dw)[XW], int lane) {
+    constexpr int QW = QEntry<XW, RW>::QW;
+    int slot = 0;
+    if (lane == 0) slot = atomicAdd(a.q_count, 1);
+    slot = __shfl(slot, 0);
+    // uniform words into lanes 0..QW-1: 32-bit selects (two registers in total)
+    uint32_t lo = (uint32_t)shot, hi = (uint32_t)((uint64_t)shot >> 32);
+#pragma unroll
+    for (int w = 0; w < XW; ++w) {
+        lo = lane == 1 + w ? (uint32_t)xw[w] : lo;
+        hi = lane == 1 + w ? (uint32_t)(xw[w] >> 32) : hi;
+        lo = lane == 1 + XW + RW + w ? (uint32_t)dw[w] : lo;
+        hi = lane == 1 + XW + RW + w ? (uint32_t)(dw[w] >> 32) : hi;
+    }
+#pragma unroll
+    for (int w = 0; w < RW; ++w) {
+        lo = lane == 1 + XW + w ? (uint32_t)rw[w] : lo;
+        hi = lane == 1 + XW + w ? (uint32_t)(rw[w] >> 32) : hi;
+    }
+    if (lane < QW) a.q_w[(int64_t)slot * QW + lane] = ((uint64_t)hi << 32) | lo;
 }
 
 }  // namespace qdec

@@ -105,6 +105,11 @@ struct DecodeArgs {
     int64_t* q_idx;    // [B]   shot of queue slot
     uint8_t* q_x;      // [B][n] BP hard decision
     uint8_t* q_r;      // [B][m] residual syndrome
+    // packed queue (wave kernels, q_packed = 1): entry s = q_w[s*(1+XW+RW) ..]:
+    // shot index, hard decision by column (XW = n_pad/64 words), residual by
+    // check (RW = m_pad/64 words); replaces q_idx/q_x/q_r
+    int q_packed;
+    uint64_t* q_w;
     // optional timing (host side only): events recorded on the launch stream
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr

@@ -37,3 +37,24 @@ for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
                   " ".join(f"{n}={buf[i]/shots:.0f}" for i, n in enumerate(names)) +
                   f" | per-iter={buf[2]/its:.0f} | waves={int(buf[12])} ticks/wave={buf[10]/max(1,buf[12]):.0f}"
                   f" real_us/wave={buf[11]/max(1,buf[12])/100:.1f}", flush=True)
+
+# SSF kernel phases (slots 16..31)
+for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
+    dec = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, flip_sets=hx, logicals=lz)
+    syn = torch.empty((B, 108), dtype=torch.uint8, device=dev)
+    rd = torch.empty((B, 225), dtype=torch.uint8, device=dev)
+    dec.sample_storage_device(0, p, p, 1, 0, 0, B, syn, rd)
+    fail = torch.empty(B, dtype=torch.uint8, device=dev)
+    dec.decode_device(B, syn=syn, readout=rd, fail=fail)
+    torch.cuda.synchronize()
+    buf = np.zeros(64, np.uint64)
+    lib.qd_dev_read_stamps(buf.ctypes.data, 64, 1)
+    dec.decode_device(B, syn=syn, readout=rd, fail=fail)
+    torch.cuda.synchronize()
+    lib.qd_dev_read_stamps(buf.ctypes.data, 64, 1)
+    b = buf[16:32]
+    shots, steps = int(b[7]), int(b[6])
+    if shots:
+        print(f"SSF p={p} shots={shots} steps/shot={steps/shots:.2f} listed/step={b[5]/max(1,steps):.1f} per-step ticks: "
+              f"gather+compact={b[0]/steps:.0f} score={b[1]/steps:.0f} select={b[2]/steps:.0f} apply={b[3]/steps:.0f} | "
+              f"per-shot: load={b[12]/shots:.0f} tail={b[13]/shots:.0f} finalize={b[14]/shots:.0f}", flush=True)
