@@ -272,10 +272,7 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
             int bad = 0;
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
-                uint64_t acc = 0;  // xor of the masked words: (X & M) ^ acc is one v_bitop3 per dword
-#pragma unroll
-                for (int w = 0; w < RV; ++w) acc ^= smask[rc][w] & X[w];
-                pres[rc] = (sbit[rc] ^ __popcll(acc)) & 1;
+                pres[rc] = sbit[rc] ^ masked_parity<RV>(smask[rc], X);  // one v_bitop3 per dword
                 bad |= pres[rc];
             }
             wave_lds_sync();  // v2c scatter complete before the next check pass

@@ -40,6 +40,19 @@ static __device__ unsigned long long qdec_stamps[64];
     } while (0)
 #endif
 
+// Parity of popc(X & M) over NW 64-bit words, X wave-uniform (ballot words).
+// Folded as two 32-bit xor-accumulators so each step is one (a & b) ^ c VALU.
+template <int NW>
+__device__ __forceinline__ int masked_parity(const uint64_t (&M)[NW], const uint64_t (&X)[NW]) {
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        lo ^= (uint32_t)M[w] & (uint32_t)X[w];
+        hi ^= (uint32_t)(M[w] >> 32) & (uint32_t)(X[w] >> 32);
+    }
+    return __builtin_popcount(lo ^ hi) & 1;
+}
+
 // Orders this wave's LDS accesses across lanes.  A wave's LDS operations
 // execute in issue order, so for a one-wave workgroup (or a wave working on its
 // own LDS region) it is enough to keep the compiler from moving them; unlike
