@@ -230,10 +230,10 @@ def main():
                        "parallelism": f"shot-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "bp_wave_kernel<float, 1, 2, 4, 7, true> (BP min-sum, fp32, queues BP failures)",
+                         "kernel": "bp_ms_wave_kernel<float, 2, 4, 7, true, true, 2> (BP min-sum, fp32, lean outputs, queues BP failures)",
                          "avg_launch_ms": float(launch_ms.mean()),
                          "launches": int(launch_ms.size),
-                         "ssf_kernel": "ssf_wave_kernel<2>", "ssf_avg_launch_ms": float(ssf_ms.mean()),
+                         "ssf_kernel": "ssf_wave_kernel<2, 4, 2>", "ssf_avg_launch_ms": float(ssf_ms.mean()),
                          "timing": "HIP events recorded by the library on the launch stream around each kernel",
                          "algorithmic_bytes_per_launch": float(bytes_per_launch.mean()),
                          "bytes_model": "per shot: (m+n+1)=334 B I/O + 16*E=12096 B per BP iteration"},

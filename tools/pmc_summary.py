@@ -52,7 +52,7 @@ def main():
             d["hbm_write_bytes_per_dispatch"] = wr
             d["hbm_bytes_per_dispatch"] = rd + wr
         kernels[k] = d
-    bp = [k for k in kernels if family(k) in ("bp_wave_kernel", "bp_block_kernel")]
+    bp = [k for k in kernels if family(k) in ("bp_wave_kernel", "bp_ms_wave_kernel", "bp_block_kernel")]
     ssf = [k for k in kernels if family(k) in ("ssf_wave_kernel", "ssf_block_kernel")]
 
     def pick(names):
