@@ -83,6 +83,10 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
     using V2 = __attribute__((ext_vector_type(2))) T;
     using Io = ShotIo<RC, RV>;
     constexpr int DRS = MsLds<T>::DRS;
+    // the variable pass runs rounds in pairs (2p, 2p+1) on packed fp32 pairs;
+    // an odd last round pairs with itself.  D3P: leading 3-edge rounds, whole pairs.
+    constexpr int NP = (RV + 1) / 2;
+    constexpr int D3P = D3R & ~1;
     constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* v2c = reinterpret_cast<T*>(smem);
@@ -95,14 +99,15 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
     const T* prior = reinterpret_cast<const T*>(g.ms_prior[PREC]);
 
     uint32_t etab[RV][kDC];  // v2c element | state index << 16 (edges k < kd(rv))
-    T L[RV];
+    V2 L[NP];                // priors of rounds (2p, 2p+1)
     uint32_t vsl[(RV + 1) / 2];  // columns of this lane's slots, u16 pairs
 #pragma unroll
     for (int rv = 0; rv < RV; ++rv) {
         const int sl = rv * 64 + lane;
-        L[rv] = prior[sl];
+        if (rv % 2 == 0) L[rv / 2].x = L[rv / 2].y = prior[sl];
+        else L[rv / 2].y = prior[sl];
 #pragma unroll
-        for (int k = 0; k < kDC; ++k) etab[rv][k] = (rv < D3R && k == 3) ? 0u : g.ms_etab[PREC][k * g.n_pad + sl];
+        for (int k = 0; k < kDC; ++k) etab[rv][k] = (rv < D3P && k == 3) ? 0u : g.ms_etab[PREC][k * g.n_pad + sl];
         if (rv % 2 == 0) vsl[rv / 2] = g.ms_vslot[sl];
         else vsl[rv / 2] |= (uint32_t)g.ms_vslot[sl] << 16;
     }
@@ -135,12 +140,12 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
         Io::patch_tail(a.syn, a.B, m, shot, io.syn, io.syn_shift, lane);
         wave_lds_sync();
         QDEC_STAMP(0);
-        int sbit[RC];
+        bool sbit[RC];  // lane masks: parity work stays on the scalar unit
         const uint8_t* srow = io.syn_row();
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) {
             const int i = rc * 64 + lane;
-            sbit[rc] = (i < m && a.syn) ? (int)(srow[i] & 1) : 0;
+            sbit[rc] = (i < m && a.syn) ? (srow[i] & 1) != 0 : false;
         }
         wait_lds();
         io.stage(g, a, shot + gridDim.x, buf ^ 1, lane);
@@ -163,25 +168,27 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                 uint64_t acc = 0;
 #pragma unroll
                 for (int w = 0; w < RV; ++w) acc ^= smask[rc][w] & Xf[w];
-                sbit[rc] ^= __popcll(acc) & 1;
+                sbit[rc] ^= (__popcll(acc) & 1) != 0;
             }
         }
 
         // ---- initial messages: v2c = prior ----
-        T vp[RV][kDC];
+        V2 vp[NP][kDC];  // v2c messages this lane sent last iteration, round pairs
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int k = 0; k < kDC; ++k) vp[p][k] = L[p];
 #pragma unroll
         for (int rv = 0; rv < RV; ++rv)
 #pragma unroll
-            for (int k = 0; k < kDC; ++k) {
-                vp[rv][k] = L[rv];
-                if (!(rv < D3R && k == 3)) v2c[etab[rv][k] & 0xffff] = L[rv];
-            }
+            for (int k = 0; k < kDC; ++k)
+                if (!(rv < D3P && k == 3)) v2c[etab[rv][k] & 0xffff] = (rv % 2 == 0) ? L[rv / 2].x : L[rv / 2].y;
         wave_lds_sync();
 
         QDEC_STAMP(1);
         T Q[RV];
         uint64_t X[RV];
-        int pres[RC];
+        bool pres[RC];
         int it = 1;
         bool conv = false;
         for (; it <= a.max_iter; ++it) {
@@ -193,7 +200,7 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                 T v[kDR];
                 lds_load<T, kDR>(v2c + i * DRS, v);
                 T m1 = Big<T>::v, m2 = Big<T>::v;
-                int par = sbit[rc];
+                bool par = sbit[rc];
 #pragma unroll
                 for (int k = 0; k < DRC; ++k) {
                     const T av = fabs(v[k]);
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                         m1 = med3(av, m1, -Big<T>::v);  // true median = min(|v|, m1): one VALU, abs modifier
                     else
                         m1 = fmin(m1, av);
-                    par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign
+                    par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign (s_xor of compare masks)
                 }
                 // both minima carry the parity in their sign bit (they are >= +0)
                 V2 s2;
@@ -212,38 +219,46 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
             }
             wave_lds_sync();
 
-            // ---- variable pass (states of round rv+1 in flight while rv computes) ----
-            V2 sn[kDC];
+            // ---- variable pass, rounds in pairs (the next pair's states are
+            // gathered while this pair sums) ----
+            auto gather = [&](int p, V2 (&sa)[kDC], V2 (&sb)[kDC]) {
+                const int r0 = 2 * p, r1 = 2 * p + 1 < RV ? 2 * p + 1 : 2 * p;
 #pragma unroll
-            for (int k = 0; k < kDC; ++k)
-                if (!(0 < D3R && k == 3)) sn[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[0][k] >> 16));
+                for (int k = 0; k < kDC; ++k)
+                    if (!(r1 < D3P && k == 3)) {
+                        sa[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[r0][k] >> 16));
+                        if (r1 != r0) sb[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[r1][k] >> 16));
+                    }
+            };
+            V2 sa[kDC], sb[kDC];
+            gather(0, sa, sb);
 #pragma unroll
-            for (int rv = 0; rv < RV; ++rv) {
-                constexpr int kd4 = kDC;
-                const int KD = rv < D3R ? 3 : kd4;
-                V2 sc[kDC];
-#pragma unroll
-                for (int k = 0; k < kDC; ++k) sc[k] = sn[k];
-                if (rv + 1 < RV) {
-#pragma unroll
-                    for (int k = 0; k < kDC; ++k)
-                        if (!(rv + 1 < D3R && k == 3))
-                            sn[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[rv + 1 < RV ? rv + 1 : rv][k] >> 16));
-                }
+            for (int p = 0; p < NP; ++p) {
+                const int r0 = 2 * p, r1 = 2 * p + 1 < RV ? 2 * p + 1 : 2 * p;
+                const int KD = r1 < D3P ? 3 : kDC;
                 // |c| = alpha * ((|v| == m1) ? m2 : m1), sign = parity ^ (v <= 0);
                 // the state's signs carry the parity, so one select picks both
-                T c[kDC];
+                V2 y[kDC];
 #pragma unroll
                 for (int k = 0; k < kDC; ++k) {
                     if (k < KD) {
-                        const V2 s2 = sc[k];
-                        const T v = vp[rv][k];
-                        const T y = ((fabs(v) == fabs(s2.x)) ? s2.y : s2.x) * alpha;
-                        c[k] = (v <= (T)0) ? -y : y;
+                        y[k].x = (fabs(vp[p][k].x) == fabs(sa[k].x)) ? sa[k].y : sa[k].x;
+                        const V2 sbk = r1 != r0 ? sb[k] : sa[k];
+                        y[k].y = (fabs(vp[p][k].y) == fabs(sbk.x)) ? sbk.y : sbk.x;
                     }
                 }
-                T pre[kDC];
-                T acc = L[rv];
+                if (p + 1 < NP) gather(p + 1 < NP ? p + 1 : p, sa, sb);
+                V2 c[kDC];
+#pragma unroll
+                for (int k = 0; k < kDC; ++k) {
+                    if (k < KD) {
+                        const V2 yk = y[k] * alpha;
+                        c[k].x = (vp[p][k].x <= (T)0) ? -yk.x : yk.x;
+                        c[k].y = (vp[p][k].y <= (T)0) ? -yk.y : yk.y;
+                    }
+                }
+                V2 pre[kDC];
+                V2 acc = L[p];
 #pragma unroll
                 for (int k = 0; k < kDC; ++k) {
                     if (k < KD) {
@@ -251,19 +266,24 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
                         acc += c[k];
                     }
                 }
-                if constexpr (!LEAN) Q[rv] = acc;
-                X[rv] = __ballot(acc <= (T)0);
+                if constexpr (!LEAN) {
+                    Q[r0] = acc.x;
+                    Q[r1] = acc.y;
+                }
+                X[r0] = __ballot(acc.x <= (T)0);
+                if (r1 != r0) X[r1] = __ballot(acc.y <= (T)0);
                 // ldpc: out_k = pre_k + (sum of the later c); the last one adds an
                 // empty sum (+0), which can only turn -0 into +0: both are <= 0 and
                 // have |v| = 0, so the message is used identically either way
-                T suf = (T)0;
+                V2 suf;
 #pragma unroll
                 for (int k = kDC - 1; k >= 0; --k) {
                     if (k < KD) {
-                        const T out = (k == KD - 1) ? pre[k] : pre[k] + suf;
+                        const V2 out = (k == KD - 1) ? pre[k] : pre[k] + suf;
                         suf = (k == KD - 1) ? c[k] : suf + c[k];
-                        vp[rv][k] = out;
-                        v2c[etab[rv][k] & 0xffff] = out;  // pads -> dummy element
+                        vp[p][k] = out;
+                        v2c[etab[r0][k] & 0xffff] = out.x;  // pads -> dummy element
+                        if (r1 != r0) v2c[etab[r1][k] & 0xffff] = out.y;
                     }
                 }
             }
@@ -272,7 +292,7 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
             int bad = 0;
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
-                pres[rc] = sbit[rc] ^ masked_parity<RV>(smask[rc], X);  // one v_bitop3 per dword
+                pres[rc] = sbit[rc] != (masked_parity<RV>(smask[rc], X) != 0);
                 bad |= pres[rc];
             }
             wave_lds_sync();  // v2c scatter complete before the next check pass

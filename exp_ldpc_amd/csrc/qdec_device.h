@@ -41,14 +41,16 @@ static __device__ unsigned long long qdec_stamps[64];
 #endif
 
 // Parity of popc(X & M) over NW 64-bit words, X wave-uniform (ballot words).
-// Folded as two 32-bit xor-accumulators so each step is one (a & b) ^ c VALU.
+// Two 32-bit accumulators, each step acc = (M & X) ^ acc as one v_bitop3_b32
+// (table 0x6c = (src0 & src2) ^ src1); written as the builtin so the xor chain
+// is not reassociated into and/and/xor triples.
 template <int NW>
 __device__ __forceinline__ int masked_parity(const uint64_t (&M)[NW], const uint64_t (&X)[NW]) {
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-        lo ^= (uint32_t)M[w] & (uint32_t)X[w];
-        hi ^= (uint32_t)(M[w] >> 32) & (uint32_t)(X[w] >> 32);
+        lo = __builtin_amdgcn_bitop3_b32((uint32_t)M[w], lo, (uint32_t)X[w], 0x6c);
+        hi = __builtin_amdgcn_bitop3_b32((uint32_t)(M[w] >> 32), hi, (uint32_t)(X[w] >> 32), 0x6c);
     }
     return __builtin_popcount(lo ^ hi) & 1;
 }
