@@ -105,8 +105,8 @@ class QuantumCodeLogicals:
 
     @staticmethod
     def empty(num_qubits: int) -> "QuantumCodeLogicals":
-        return QuantumCodeLogicals(np.zeros((0, num_qubits), dtype=np.int32),
-                                   np.zeros((0, num_qubits), dtype=np.int32))
+        return QuantumCodeLogicals(np.zeros((0, num_qubits), dtype=np.uint32),
+                                   np.zeros((0, num_qubits), dtype=np.uint32))
 
 
 @dataclass(frozen=True, init=False)

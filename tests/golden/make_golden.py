@@ -177,5 +177,38 @@ def main():
     print("done")
 
 
+GRAPH_SEEDS = [0x59824c5a, 0x9dca707a, 0xe0218aa8, 0x81da8035]  # first seeds of tests/test_random_biregular_graph.py:21
+GRAPH_SHAPES = [(27, 3, 4), (10, 5, 6), (21, 7, 8), (27, 9, 10)]   # (left vertices, right degree, left degree), :28-33
+
+
+def graphs():
+    """Edge lists of the reference's random_biregular_graph / remove_short_cycles on
+    the shapes its own tests use, plus the C4 code (biregular_hgp(80,3,4), n=10^4)
+    checks.  Output: graphs.npz, hgp_80_3_4_s2025_checks.npz."""
+    sys.path.insert(0, REPO)
+    _import_reference()
+    from qldpc import biregular_hgp, random_biregular_graph, remove_short_cycles
+    out = {}
+    for (lv, rdeg, ldeg) in GRAPH_SHAPES:
+        for s in GRAPH_SEEDS:
+            g = random_biregular_graph(lv, lv * ldeg // rdeg, rdeg, ldeg, seed=s)
+            out[f"rbg_{lv}_{rdeg}_{ldeg}_{s}"] = np.array(sorted((min(u, v), max(u, v)) for u, v in g.edges()),
+                                                          dtype=np.int64)
+    for s in GRAPH_SEEDS[:2]:  # tests/test_random_biregular_graph.py:41-53
+        g = random_biregular_graph(102, 102 * 4 // 3, 3, 4, seed=s)
+        remove_short_cycles(g, 4, seed=s - 42, patience=10000)
+        out[f"girth4_102_3_4_{s}"] = np.array(sorted((min(u, v), max(u, v)) for u, v in g.edges()), dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "graphs.npz"), **out)
+    code = biregular_hgp(80, 3, 4, seed=2025, compute_logicals=False)
+    arrs = {}
+    arrs.update(_csr_dict("hx", code.checks.x))
+    arrs.update(_csr_dict("hz", code.checks.z))
+    np.savez_compressed(os.path.join(HERE, "hgp_80_3_4_s2025_checks.npz"), **arrs)
+    print("graphs done:", len(out), "graphs; C4 code", code.checks.z.shape, code.checks.z.nnz)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--graphs":
+        graphs()
+    else:
+        main()
