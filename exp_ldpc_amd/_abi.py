@@ -67,6 +67,8 @@ SIGNATURES = {
     "qd_osd_last_error": (C.c_char_p, []),
     "qd_graph_set_timing": (_i32, [_p, _i32]),
     "qd_graph_read_timing": (_i32, [_p, _p, _p, _i32, C.POINTER(_i32)]),
+    "qd_gf2_rref": (_i64, [_p, _i64, _i64, _i64, _p, _i32]),
+    "qd_gf2_extend_basis": (_i64, [_p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64]),
 }
 
 

@@ -8,9 +8,14 @@ from this image) for the two jobs the decoding path needs:
   ``null_space`` / ``column_space`` / ``row_reduce``), and
 * ranks for test assertions (reference ``get_rank``, ``python/qldpc/linalg.py:98-99``).
 
-Rows are packed little-endian into uint64 words so elimination on n ~ 10^4 columns
-stays fast in numpy.  Nothing here runs on the GPU: it produces fixtures and the
-dense ``Lz`` table that the logical-check kernel consumes.
+Rows are packed little-endian into uint64 words.  The elimination itself runs in
+the host library (``qd_gf2_rref`` / ``qd_gf2_extend_basis``,
+``csrc/qdec_gf2.cpp``, threaded over rows) when ``libqdec_hip.so`` is built --
+it loads without a GPU -- so the 10^4..5*10^4-qubit codes of BASELINE configs 4
+and 5 get their logicals in seconds; a numpy loop is kept for environments
+without the library (code construction is offline tooling, not the decode
+path).  Nothing here runs on the GPU: it produces fixtures and the dense ``Lz``
+table that the logical-check kernel consumes.
 """
 from __future__ import annotations
 
@@ -49,16 +54,25 @@ def _bit(p: np.ndarray, col: int) -> np.ndarray:
     return (p[:, col >> 6] >> np.uint64(col & 63)) & np.uint64(1)
 
 
-def row_reduce(a, ncols: int | None = None):
-    """Reduced row echelon form over GF(2).
+def _native():
+    try:
+        from . import _abi
+        return _abi.load()
+    except Exception:
+        return None
 
-    Pivots are searched in columns ``0 .. ncols-1`` (all columns by default).
-    Returns ``(rref_dense, pivot_columns)`` with zero rows dropped.
-    """
-    a = np.asarray(a) % 2
-    r, n = a.shape
-    limit = n if ncols is None else ncols
-    p = pack_rows(a)
+
+def _rref_packed(p: np.ndarray, n: int, limit: int):
+    """In-place RREF of packed rows over columns [0, limit); returns (rank, pivots)."""
+    lib = _native()
+    r = p.shape[0]
+    if lib is not None and r and p.shape[1]:
+        p = np.ascontiguousarray(p)
+        piv = np.zeros(max(r, 1), dtype=np.int64)
+        rank = int(lib.qd_gf2_rref(p.ctypes.data, r, p.shape[1], limit, piv.ctypes.data, 0))
+        if rank < 0:
+            raise ValueError("qd_gf2_rref: bad arguments")
+        return p, rank, piv[:rank].copy()
     pivots = []
     row = 0
     for col in range(limit):
@@ -77,7 +91,20 @@ def row_reduce(a, ncols: int | None = None):
             p[mask] ^= p[row]
         pivots.append(col)
         row += 1
-    return unpack_rows(p[:row], n), np.array(pivots, dtype=np.int64)
+    return p, row, np.array(pivots, dtype=np.int64)
+
+
+def row_reduce(a, ncols: int | None = None):
+    """Reduced row echelon form over GF(2).
+
+    Pivots are searched in columns ``0 .. ncols-1`` (all columns by default).
+    Returns ``(rref_dense, pivot_columns)`` with zero rows dropped.
+    """
+    a = np.asarray(a) % 2
+    r, n = a.shape
+    limit = n if ncols is None else ncols
+    p, rank, piv = _rref_packed(pack_rows(a), n, limit)
+    return unpack_rows(p[:rank], n), piv
 
 
 def rank(a) -> int:
@@ -108,7 +135,19 @@ def homology_representatives(image_rows, kernel_rows) -> np.ndarray:
     [image; kernel] and keep the kernel rows that add a pivot)."""
     image_rows = np.asarray(image_rows) % 2
     kernel_rows = np.asarray(kernel_rows) % 2
-    img, _ = row_reduce(image_rows)
+    img, img_piv = row_reduce(image_rows)
+    lib = _native()
+    if lib is not None and kernel_rows.shape[0]:
+        # reduce each kernel vector against rref(image) + the vectors kept so far
+        n = kernel_rows.shape[1]
+        pb, pk = pack_rows(img) if img.shape[0] else np.zeros((0, (n + 63) // 64), np.uint64), pack_rows(kernel_rows)
+        acc = np.zeros(kernel_rows.shape[0], dtype=np.uint8)
+        lead = np.ascontiguousarray(img_piv, dtype=np.int64)
+        got = lib.qd_gf2_extend_basis(pb.ctypes.data, pb.shape[0], lead.ctypes.data, pk.ctypes.data, pk.shape[0],
+                                      pk.shape[1], n, acc.ctypes.data, -1)
+        if got < 0:
+            raise ValueError("qd_gf2_extend_basis: bad arguments")
+        return kernel_rows[acc.astype(bool)]
     # Columns of the augmented matrix [img^T | ker^T]: pivots beyond img's rank
     # pick the kernel vectors outside span(img).
     aug = np.hstack([img.T, kernel_rows.T])
@@ -123,7 +162,9 @@ def pair_logicals(z_logicals, x_logicals) -> np.ndarray:
     z = np.asarray(z_logicals) % 2
     x = np.asarray(x_logicals) % 2
     k = x.shape[0]
-    inner = (z.astype(np.int64) @ x.T.astype(np.int64)) % 2
+    # BLAS float32 product: exact, every partial sum is an integer <= n < 2^24
+    assert z.shape[1] < (1 << 24)
+    inner = (z.astype(np.float32) @ x.T.astype(np.float32)).astype(np.int64) % 2
     aug = np.hstack([inner, z]).astype(np.uint8)
     red, _ = row_reduce(aug, ncols=k)
     return red[:, k:]

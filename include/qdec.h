@@ -145,6 +145,22 @@ int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_c
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */
 int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream);
 
+/* GF(2) elimination on bit-packed rows (uint64 words, bit j at word j/64), host
+ * cores.  Offline code-construction support for the logical operators the fused
+ * failure check consumes; replaces galois row_reduce / null_space /
+ * column_space in the reference's get_logicals
+ * (python/qldpc/homological_product_code.py:6-60).
+ * qd_gf2_rref: in-place reduced row echelon form over columns [0, ncols); the
+ * first `rank` rows are the pivot rows, pivots[r] = their pivot columns
+ * (nullable).  Returns rank, or < 0 on bad arguments.
+ * qd_gf2_extend_basis: reduce each candidate row against an echelon basis (row b
+ * has its lowest set bit at basis_lead[b]) plus the candidates accepted so far;
+ * accepted[c] = 1 for candidates outside that span (at most max_accept when >= 0).
+ * Returns the number accepted (homological_product_code.py:15-21). */
+int64_t qd_gf2_rref(uint64_t* rows, int64_t nrows, int64_t words, int64_t ncols, int64_t* pivots, int32_t nthreads);
+int64_t qd_gf2_extend_basis(const uint64_t* basis, int64_t nbasis, const int64_t* basis_lead, const uint64_t* cand,
+                            int64_t ncand, int64_t words, int64_t ncols, uint8_t* accepted, int64_t max_accept);
+
 #ifdef __cplusplus
 }
 #endif
