@@ -583,7 +583,7 @@ int qd_graph_set_logicals(qd_graph* G, int32_t k, const uint8_t* lz) {
         set_device(G);
         DevGraph& g = G->dg;
         if (k < 0 || (k > 0 && !lz)) throw Fail(-40, "invalid logicals");
-        if (k > 256) throw Fail(-41, "more than 256 logicals not supported by this build");
+        if (k > 65536) throw Fail(-41, "more than 65536 logicals not supported");
         const int W = g.lz_words;
         std::vector<uint64_t> packed((size_t)std::max(k, 1) * W, 0);
         for (int r = 0; r < k; ++r)

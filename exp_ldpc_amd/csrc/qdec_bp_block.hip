@@ -89,19 +89,38 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
     __syncthreads();
 }
 
+// control area + xh + one or two m_pad byte arrays + logical parities
+__host__ __device__ inline size_t block_small_lds(const DevGraph& g) {
+    return kCtrl + (size_t)g.n_pad + 2 * (size_t)g.m_pad + 4 * (size_t)(g.k > 0 ? g.k : 1);
+}
+
+// Bytes of one workgroup's HBM scratch slice: the messages and/or the per-shot
+// byte arrays that do not fit the LDS budget (placement bits as in bp_block_kernel).
+__host__ __device__ inline size_t block_slice_bytes(const DevGraph& g, size_t tsz, int placement) {
+    size_t b = 0;
+    if (!(placement & 1)) b += ((size_t)2 * g.E * tsz + 15) / 16 * 16;
+    if (!(placement & 2)) b += (block_small_lds(g) + 255) / 256 * 256;
+    return (b + 255) / 256 * 256;
+}
+
 template <typename T, int METHOD, bool DEFER>
-__global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs a, T* gscratch, int msgs_in_lds) {
+__global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs a, T* gscratch, int placement) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int E = g.E, m = g.m, n = g.n, tid = threadIdx.x;
     constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
     int* slot_s = reinterpret_cast<int*>(smem + 48);
-    unsigned char* p = smem + kCtrl;
+    // placement bit 0: messages in LDS, bit 1: per-shot byte arrays in LDS;
+    // whatever is not in LDS lives in this workgroup's HBM scratch slice
+    const size_t msg_bytes = ((size_t)2 * E * sizeof(T) + 15) / 16 * 16;
+    unsigned char* slice = reinterpret_cast<unsigned char*>(gscratch) +
+                           (size_t)blockIdx.x * block_slice_bytes(g, sizeof(T), placement);
+    unsigned char* p = (placement & 2) ? smem + kCtrl : slice + ((placement & 1) ? 0 : msg_bytes);
     T* v2c;
-    if (msgs_in_lds) {
+    if (placement & 1) {
         v2c = reinterpret_cast<T*>(p);
-        p += ((size_t)2 * E * sizeof(T) + 15) / 16 * 16;
+        p += msg_bytes;
     } else {
-        v2c = gscratch + (size_t)blockIdx.x * 2 * E;
+        v2c = reinterpret_cast<T*>(slice);
     }
     T* c2v = v2c + E;
     uint8_t* xh = p;                      // [n_pad]
@@ -330,24 +349,30 @@ static int launch_block2(K kern, size_t lds, int64_t work, int num_cus, hipStrea
     return (int)hipGetLastError();
 }
 
-// control area + xh + one or two m_pad byte arrays + logical parities
-size_t block_small_lds(const DevGraph& g) {
-    return kCtrl + (size_t)g.n_pad + 2 * (size_t)g.m_pad + 4 * (size_t)(g.k > 0 ? g.k : 1);
-}
-
 constexpr size_t kLdsMsgLimit = 64 * 1024;  // messages in LDS up to this (2 workgroups per CU)
+
+// Where the BP workgroup keeps its state: messages in LDS when everything fits
+// kLdsMsgLimit, else in HBM; the per-shot byte arrays stay in LDS up to
+// kLdsMsgLimit (n ~ 6*10^4), beyond that (e.g. the 1.2*10^5-column spacetime
+// graph of config 5) they move to the HBM slice as well.
+inline int block_placement(const DevGraph& g, size_t tsz) {
+    const size_t msg = ((size_t)2 * g.E * tsz + 15) / 16 * 16;
+    const size_t small = (block_small_lds(g) + 15) / 16 * 16;
+    if (msg + small <= kLdsMsgLimit) return 3;
+    return small <= kLdsMsgLimit ? 2 : 0;
+}
 
 template <typename T, int METHOD>
 static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, void* scratch,
                               size_t scratch_bytes) {
     const size_t msg = ((size_t)2 * g.E * sizeof(T) + 15) / 16 * 16;
     const size_t small = (block_small_lds(g) + 15) / 16 * 16;
-    const bool in_lds = msg + small <= kLdsMsgLimit;
-    const size_t lds = small + (in_lds ? msg : 0);
+    const int placement = block_placement(g, sizeof(T));
+    const size_t lds = (placement & 2) ? small + ((placement & 1) ? msg : 0) : kCtrl;
     int cap = 0;
-    if (!in_lds) {
-        // per-workgroup message slices in HBM scratch
-        const size_t per_wg = (size_t)2 * g.E * sizeof(T);
+    if (placement != 3) {
+        // per-workgroup slices in HBM scratch
+        const size_t per_wg = block_slice_bytes(g, sizeof(T), placement);
         if (!scratch || per_wg == 0) return (int)hipErrorInvalidValue;
         const long long max_wg = (long long)(scratch_bytes / per_wg);
         if (max_wg < 1) return (int)hipErrorOutOfMemory;
@@ -356,7 +381,7 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     T* gs = reinterpret_cast<T*>(scratch);
     if (!a.ssf) {
         record_ev(a, 0, stream);
-        const int rc = launch_block(bp_block_kernel<T, METHOD, false>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+        const int rc = launch_block(bp_block_kernel<T, METHOD, false>, lds, a.B, num_cus, stream, cap, g, a, gs, placement);
         record_ev(a, 1, stream);
         record_ev(a, 2, stream);
         return rc;
@@ -365,7 +390,8 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
     if (e != hipSuccess) return (int)e;
     record_ev(a, 0, stream);
-    int rc = launch_block(bp_block_kernel<T, METHOD, true>, lds, a.B, num_cus, stream, cap, g, a, gs, in_lds);
+    if (!(placement & 2)) return (int)hipErrorNotSupported;  // SSF keeps its shot state in LDS
+    int rc = launch_block(bp_block_kernel<T, METHOD, true>, lds, a.B, num_cus, stream, cap, g, a, gs, placement);
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
     rc = launch_block2(ssf_block_kernel, small, a.B, num_cus, stream, g, a);
@@ -375,10 +401,9 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
 
 size_t block_scratch_bytes(const DevGraph& g, int precision, int num_cus) {
     const size_t tsz = precision == 1 ? 4 : 8;
-    const size_t msg = ((size_t)2 * g.E * tsz + 15) / 16 * 16;
-    const size_t small = (block_small_lds(g) + 15) / 16 * 16;
-    if (msg + small <= kLdsMsgLimit) return 0;
-    return (size_t)num_cus * 4 * (size_t)2 * g.E * tsz;  // up to 4 workgroups per CU
+    const int placement = block_placement(g, tsz);
+    if (placement == 3) return 0;
+    return (size_t)num_cus * 4 * block_slice_bytes(g, tsz, placement);  // up to 4 workgroups per CU
 }
 
 int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,

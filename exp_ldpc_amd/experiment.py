@@ -12,7 +12,9 @@ device.  Decoder modes (``--decoder_mode``):
   bpssf              BP + small-set-flip on H (R = 0); R >= 1 runs bpssf_hybrid
   bpssf_hybrid       BP on spacetime, fold, then BP+SSF on H     (build-defined)
   bp                 BP only on the spacetime matrix
-  bpd_detector       not supported (needs a Stim detector error model)
+  bpd_detector       BP on the fault check matrix of a detector error model
+                     (_experiment.py:128-151); the storage experiment's DEM is
+                     written by dem.storage_experiment_dem (R = 0 / 1)
 
 OSD runs on the host cores for the shots BP did not converge on (osd.py).
 Logical failure = any(Lz (readout + correction)) mod 2 as at _experiment.py:209
@@ -41,7 +43,7 @@ from .spacetime import SpacetimeCode, SpacetimeCodeSingleShot
 from .storage_sim import build_storage_simulation
 
 __all__ = ["DECODER_MODES", "BatchPipeline", "BPOSDCorrect", "BPOSDHybridCorrect", "BPOSDCorrectSingleShot",
-           "BPSSFCorrect", "run_simulation", "add_bposd_args", "unpack_bposd_args", "load_code", "p_sweep",
+           "BPSSFCorrect", "BPDetectorCorrect", "run_simulation", "add_bposd_args", "unpack_bposd_args", "load_code", "p_sweep",
            "p_sweep_main", "parse_sweep_spec"]
 
 DECODER_MODES = ["bposd", "bposd_single_shot", "bposd_hybrid", "bpd_detector", "bpssf", "bpssf_hybrid", "bp"]
@@ -67,10 +69,8 @@ class BatchPipeline:
     device tensors (spacetime syndrome uint8[B,(R+1)m], readout uint8[B,n])."""
 
     def __init__(self, code, rounds: int, mode: str, bp_osd_options: Dict, priors: Tuple[float, float], *,
-                 device: int = 0, precision: str = "f32", use_x_logicals: bool = False, osd_threads: int = 0):
-        if mode == "bpd_detector":
-            raise NotImplementedError("decoder_mode 'bpd_detector' needs a Stim detector error model "
-                                      "(DetectorSpacetimeCode); not supported by this build")
+                 device: int = 0, precision: str = "f32", use_x_logicals: bool = False, osd_threads: int = 0,
+                 noise=None):
         if mode not in DECODER_MODES:
             raise RuntimeError("Unknown decoder operation mode")
         if mode == "bpssf" and rounds > 0:
@@ -116,6 +116,21 @@ class BatchPipeline:
             prior[n:] = meas_prior
             self.ss = Decoder(Hss, prior, n_data=n, fold_blocks=1, **common)
             self.ss_osd = OsdSolver(Hss, osd_method, osd_order, osd_threads)
+        if mode == "bpd_detector":
+            # reference BPDetectorCorrect (_experiment.py:128-151): BP (no OSD) on the
+            # DEM's fault check matrix with its fault priors.  The sampler's
+            # spacetime syndrome is the DEM's detector vector; the readout-flip
+            # faults (the DEM's last n columns) carry fault-map columns Lz[:, j], so
+            # the readout placed there reproduces the observables and the fused
+            # check any(F (v ^ x)) = any(obs ^ F x) is the reference's failure flag.
+            if noise is None or getattr(noise, "kind", "") != "depolarizing":
+                raise NotImplementedError("bpd_detector builds its DEM for depolarizing_noise(p, pm) only")
+            from .dem import DetectorSpacetimeCode, storage_experiment_dem
+            self.dem = DetectorSpacetimeCode(storage_experiment_dem(self.H, self.L, R, noise.p, noise.pm))
+            fmap = self.dem.fault_map.toarray() % 2
+            self.n_faults = self.dem.fault_priors.size
+            self.det = Decoder(self.dem.fault_check_matrix, self.dem.fault_priors,
+                               logicals=fmap if fmap.shape[0] else None, **common)
         # a plain-H decoder for the sampler
         self.sampler_graph = Decoder(self.H, 0.01, device=self.device)
 
@@ -185,6 +200,10 @@ class BatchPipeline:
         elif mode == "bpssf":
             self.fin.decode_device(B, syn=syn, readout=readout, corr=corr, iters=iters, status=status,
                                    ssf_steps=steps, fail=fail)
+        elif mode == "bpd_detector":
+            v = torch.zeros((B, self.n_faults), **u8)
+            v[:, self.n_faults - n:] = readout
+            self.det.decode_device(B, syn=syn, readout=v, iters=iters, status=status, fail=fail)
         elif mode == "bposd_single_shot":
             acc = torch.zeros((B, n), **u8)
             raw = torch.zeros((B, m), **u8)
@@ -276,6 +295,28 @@ class BPSSFHybridCorrect(_PerShot):
     mode = "bpssf_hybrid"
 
 
+class BPDetectorCorrect:
+    """Reference ``BPDetectorCorrect`` (_experiment.py:128-151): BP on the fault
+    check matrix of a detector error model (DEM text or dem.DetectorErrorModel);
+    ``readout_correction(detector_string)`` returns the corrected observables."""
+
+    def __init__(self, detector_error_model, bp_osd_options: Dict, *, device: int = 0, precision: str = "f32"):
+        from .dem import DetectorSpacetimeCode
+        self._detector_spacetime_code = DetectorSpacetimeCode(detector_error_model)
+        o = bp_osd_options
+        c = self._detector_spacetime_code
+        self._bpd = Decoder(c.fault_check_matrix, c.fault_priors, method=o.get("bp_method", "ps"), precision=precision,
+                            max_iter=int(o.get("max_iter", 0) or 0), ms_scaling=float(o.get("ms_scaling_factor", 0.0)),
+                            device=device)
+
+    def readout_correction(self, detector_string) -> np.ndarray:
+        c = self._detector_spacetime_code
+        d = c.fault_check_matrix.shape[0]
+        s = np.asarray(detector_string, dtype=np.uint8) % 2
+        fault_set = self._bpd.decode(s[:d][None], want=("x",))["x"][0]
+        return ((s[d:].astype(np.int64) + c.fault_map.astype(np.int64) @ fault_set) % 2).astype(np.int64)
+
+
 # ------------------------------------------------------------------ simulation
 def _steps(checks):
     def mx(a):
@@ -295,7 +336,8 @@ def run_simulation(samples, code, meas_prior, data_prior, noise_model, noise_mod
     sim = build_storage_simulation(rounds, noise_model(**noise_model_args), code, use_x_logicals=False)
     mp = meas_prior(x_steps, z_steps)
     dp = data_prior(x_steps, z_steps)
-    pipe = BatchPipeline(code, rounds, decoder_mode, bp_osd_options, (dp, mp), device=device, precision=precision)
+    pipe = BatchPipeline(code, rounds, decoder_mode, bp_osd_options, (dp, mp), device=device, precision=precision,
+                         noise=noise_model(**noise_model_args))
     out = np.zeros(samples, dtype=bool)
     agg = {"bp_converged": 0, "iters_sum": 0, "ssf_steps_sum": 0}
     with torch.cuda.device(device):
@@ -370,7 +412,7 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
         sim = build_storage_simulation(rounds, nm, code, use_x_logicals=False)
         dp = data_prior(p_ph, x_steps, z_steps)
         mp = meas_prior(p_ph, x_steps, z_steps)
-        pipes = [BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision)
+        pipes = [BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision, noise=nm)
                  for d in range(ndev)]
         per = math.ceil(samples / ndev)
         failures = conv = iters = ssf = 0

@@ -1,0 +1,135 @@
+"""GPU parity on the larger benchmark codes (BASELINE configs 3-5), built by this
+package's own code sources (exp_ldpc_amd/hgp.py, lifted.py):
+
+* C3  [[144,12,12]] bivariate-bicycle lift -> wave kernels, BP + SSF
+* C4  biregular_hgp(80,3,4,seed=2025), n = 10^4 (reference-generated fixture)
+      -> workgroup kernels with HBM message scratch, BP + SSF
+* C5  PSL(2,q) matrix lift: q = 5 (n = 2700) and q = 13 (n = 49,140), BP on Hz
+      and on the R = 1 spacetime graph (multi-round syndromes)
+
+Every output is compared bit-for-bit with the CPU oracle on the same sampled
+storage-experiment shots (min-sum LLRs within the fp tolerance of
+test_gpu_parity._cmp_llr)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import load_checks
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20250221
+KEYS_SSF = ("x", "corr", "iters", "status", "ssf_steps", "fail")
+
+
+def _decode_both(oracle_lib, H, prior, syn, *, rd=None, gens=None, lz=None, max_iter=50, method="ms",
+                 precision="f32", keys=("x", "iters", "status"), **kw):
+    from exp_ldpc_amd.decoder import Decoder
+    dec = Decoder(H, prior, method=method, precision=precision, max_iter=max_iter, flip_sets=gens, logicals=lz, **kw)
+    got = dec.decode(syn, readout=rd, want=keys)
+    ref = oracle_lib.decode(H, prior, syn, method=method, precision=precision, max_iter=max_iter,
+                            ssf=gens is not None, gens=gens, lz=lz, readout=rd, want_llr=False,
+                            ssf_impl="fast", **kw)
+    for k in keys:
+        assert np.array_equal(got[k], ref[k]), k
+    return got
+
+
+@pytest.fixture(scope="module")
+def bb144():
+    from exp_ldpc_amd.lifted import bivariate_bicycle_code
+    return bivariate_bicycle_code(12, 6, [(3, 0), (0, 1), (0, 2)], [(0, 3), (1, 0), (2, 0)], compute_logicals=True)
+
+
+@pytest.mark.parametrize("p", [0.003, 0.01, 0.03])
+def test_bb144_bp_ssf_parity(gpu_available, oracle_lib, bb144, p):
+    hx, hz, lz = bb144.checks.x, bb144.checks.z, bb144.logicals.z
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=3, shot0=0, B=3000)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, keys=KEYS_SSF)
+    if p >= 0.01:
+        assert (got["status"] & 1).mean() < 1.0  # BP failures reach SSF
+
+
+def test_bb144_device_sampler_matches_oracle(gpu_available, oracle_lib, bb144):
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    hz = bb144.checks.z
+    B = 4096
+    dec = Decoder(hz, 0.01, method="ms", precision="f32", max_iter=50)
+    syn = torch.empty((B, hz.shape[0]), dtype=torch.uint8, device="cuda:0")
+    rd = torch.empty((B, hz.shape[1]), dtype=torch.uint8, device="cuda:0")
+    dec.sample_storage_device(0, 0.02, 0.02, SEED, 1, 12345, B, syn, rd)
+    torch.cuda.synchronize()
+    rs, rr = oracle_lib.sample_storage(hz, 0, 0.02, 0.02, seed=SEED, stream=1, shot0=12345, B=B)
+    assert np.array_equal(syn.cpu().numpy(), rs) and np.array_equal(rd.cpu().numpy(), rr)
+
+
+@pytest.fixture(scope="module")
+def hgp10k():
+    from exp_ldpc_amd import gf2
+    hx, hz = load_checks("hgp_80_3_4_s2025")
+    _, lz = gf2.css_logicals(hx, hz)
+    return hx, hz, lz
+
+
+def test_hgp10k_bp_ssf_parity(gpu_available, oracle_lib, hgp10k):
+    hx, hz, lz = hgp10k
+    assert hz.shape == (4800, 10000) and lz.shape[0] == 400
+    p = 0.03
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=4, shot0=0, B=192)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=30, keys=KEYS_SSF)
+    assert got["ssf_steps"].sum() > 0
+
+
+def test_hgp10k_bp_f64_llr(gpu_available, oracle_lib, hgp10k):
+    from test_gpu_parity import _cmp_llr
+    from exp_ldpc_amd.decoder import Decoder
+    _, hz, _ = hgp10k
+    syn, _ = oracle_lib.sample_storage(hz, 0, 0.02, 0.02, seed=SEED, stream=5, shot0=0, B=96)
+    for method, precision in (("ms", "f64"), ("ps", "f64")):
+        dec = Decoder(hz, 0.0133, method=method, precision=precision, max_iter=20)
+        got = dec.decode(syn, want=("x", "llr", "iters", "status"))
+        ref = oracle_lib.decode(hz, 0.0133, syn, method=method, precision=precision, max_iter=20)
+        for k in ("x", "iters", "status"):
+            assert np.array_equal(got[k], ref[k]), (method, k)
+        _cmp_llr(got["llr"], ref["llr"], method, precision)
+
+
+@pytest.fixture(scope="module")
+def psl5():
+    from exp_ldpc_amd.lifted import psl2_lifted_product_code
+    return psl2_lifted_product_code(5, compute_logicals=True)
+
+
+def test_psl5_lift_bp_parity(gpu_available, oracle_lib, psl5):
+    hz, lz = psl5.checks.z, psl5.logicals.z
+    p = 0.02
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=6, shot0=0, B=400)
+    _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, lz=lz, max_iter=40, keys=("x", "corr", "iters", "status", "fail"))
+
+
+@pytest.fixture(scope="module")
+def psl13_hz():
+    from exp_ldpc_amd.lifted import psl2_lifted_product_code
+    return psl2_lifted_product_code(13).checks.z
+
+
+def test_psl13_lift_bp_parity(gpu_available, oracle_lib, psl13_hz):
+    hz = psl13_hz
+    assert hz.shape[1] == 49140
+    p = 0.01
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=7, shot0=0, B=48)
+    _decode_both(oracle_lib, hz, 2 * p / 3, syn, max_iter=15)
+
+
+def test_psl13_lift_spacetime_r1_parity(gpu_available, oracle_lib, psl13_hz):
+    """C5's multi-round spacetime syndromes: H_st = [blockdiag(Hz, Hz) | M]
+    (spacetime_code.py:46-75), sampled by the storage-experiment sampler at R = 1
+    and folded onto the data qubits."""
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    hz = psl13_hz
+    H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
+    p = 0.005
+    syn, rd = oracle_lib.sample_storage(hz, 1, p, p, seed=SEED, stream=8, shot0=0, B=24)
+    _decode_both(oracle_lib, H, 2 * p / 3, syn, max_iter=10, keys=("corr", "iters", "status"),
+                 n_data=hz.shape[1], fold_blocks=2)

@@ -1,0 +1,126 @@
+"""Throughput of the larger BASELINE configs on one MI355X (diagnostic; the
+driver's headline bench is bench.py = config 2).
+
+  c3  [[144,12,12]] bivariate-bicycle lift, BP min-sum fp32 (max_iter 50) + SSF
+  c4  biregular_hgp(80,3,4,seed=2025), n = 10^4, BP min-sum fp32 (max_iter 50) + SSF
+  c5  PSL(2,13) matrix lift, n = 49,140, R = 1 spacetime syndromes, BP min-sum fp32
+
+Shots are sampled on the device (storage experiment, depolarizing_noise(p, pm=p))
+before the timed region; the timed region decodes them (fused fold + logical
+check where logicals are given).  Prints one JSON line per (config, p).
+
+Usage: python tools/bench_configs.py [c3 c4 c5] [--shots N] [--p P ...]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+SEED = 20250221
+
+
+def build_config(name):
+    import scipy.sparse as sp
+    from exp_ldpc_amd import gf2
+    if name == "c3":
+        from exp_ldpc_amd.lifted import bivariate_bicycle_code
+        code = bivariate_bicycle_code(12, 6, [(3, 0), (0, 1), (0, 2)], [(0, 3), (1, 0), (2, 0)], compute_logicals=True)
+        return dict(hz=code.checks.z, hx=code.checks.x, lz=code.logicals.z, rounds=0, batch=1 << 18,
+                    ps=[0.001, 0.003, 0.01], desc="[[144,12,12]] BB lift, R=0, BP ms fp32 max_iter 50 + SSF")
+    if name == "c4":
+        from conftest import load_checks
+        hx, hz = load_checks("hgp_80_3_4_s2025")
+        _, lz = gf2.css_logicals(hx, hz)
+        return dict(hz=hz, hx=hx, lz=lz, rounds=0, batch=1 << 15, max_shots=1 << 18, ps=[0.01, 0.03],
+                    desc="biregular_hgp(80,3,4,seed=2025) n=10000, R=0, BP ms fp32 max_iter 50 + SSF")
+    if name == "c5":
+        from exp_ldpc_amd.lifted import psl2_lifted_product_code
+        hz = psl2_lifted_product_code(13).checks.z
+        return dict(hz=sp.csr_matrix(hz), hx=None, lz=None, rounds=1, batch=1 << 11, max_shots=1 << 15, ps=[0.002, 0.005],
+                    desc="PSL(2,13) matrix lift n=49140, R=1 spacetime (39312x117936), BP ms fp32 max_iter 50")
+    raise SystemExit(f"unknown config {name}")
+
+
+def run(name, shots, ps_override, reps):
+    import torch
+    import scipy.sparse as sp
+    from exp_ldpc_amd.decoder import Decoder
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    cfg = build_config(name)
+    hz = sp.csr_matrix(cfg["hz"])
+    m, n = hz.shape
+    R = cfg["rounds"]
+    H = sp.csr_matrix(SpacetimeCode(hz, R).spacetime_check_matrix) if R else hz
+    shots = min(shots, cfg.get("max_shots", shots))
+    B = min(cfg["batch"], shots)
+    nb = max(1, shots // B)
+    dev = torch.device("cuda", 0)
+    for p in (ps_override or cfg["ps"]):
+        sampler = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50)
+        dec = Decoder(H, 2 * p / 3, method="ms", precision="f32", max_iter=50, flip_sets=cfg["hx"],
+                      logicals=cfg["lz"], n_data=n, fold_blocks=R + 1)
+        syn = torch.empty((nb, B, H.shape[0]), dtype=torch.uint8, device=dev)
+        rd = torch.empty((nb, B, n), dtype=torch.uint8, device=dev)
+        for b in range(nb):
+            sampler.sample_storage_device(R, p, p, SEED, 0, b * B, B, syn[b], rd[b])
+        iters = torch.empty((nb, B), dtype=torch.int32, device=dev)
+        status = torch.empty((nb, B), dtype=torch.uint8, device=dev)
+        fail = torch.empty((nb, B), dtype=torch.uint8, device=dev)
+        ssf = torch.empty((nb, B), dtype=torch.int32, device=dev)
+        want_fail = cfg["lz"] is not None
+
+        def one_pass():
+            for b in range(nb):
+                dec.decode_device(B, syn=syn[b], readout=rd[b] if want_fail else None, iters=iters[b],
+                                  status=status[b], fail=fail[b] if want_fail else None, ssf_steps=ssf[b])
+        one_pass()  # warmup
+        torch.cuda.synchronize()
+        dec.set_timing(nb * reps)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            one_pass()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        bp_ms, ssf_ms = dec.read_timing()
+        E = int(H.nnz)
+        it_sum = float(iters.to(torch.int64).sum().item())
+        io = H.shape[0] + n + 1
+        bytes_per_pass = io * B * nb + 16 * E * it_sum
+        kernel_s = bp_ms.sum() / 1e3 / reps
+        total = nb * B * reps
+        res = {
+            "config": name, "desc": cfg["desc"], "p": p, "shots": total, "shots_per_s": total / dt,
+            "ms_per_pass": dt / reps * 1e3, "batch": B,
+            "bp_converged_frac": float((status & 1).to(torch.float64).mean().item()),
+            "mean_bp_iters": it_sum / (nb * B), "mean_ssf_steps": float(ssf.to(torch.float64).mean().item()),
+            "ler": float(fail.to(torch.float64).mean().item()) if want_fail else None,
+            "bp_kernel_ms_per_launch": float(bp_ms.mean()), "ssf_kernel_ms_per_launch": float(ssf_ms.mean()),
+            "E": E, "algorithmic_GBps_bp_kernel": bytes_per_pass / kernel_s / 1e9,
+        }
+        print(json.dumps(res), flush=True)
+        del syn, rd
+        torch.cuda.empty_cache()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5"])
+    ap.add_argument("--shots", type=int, default=1 << 20, help="distinct shots per p (rounded to batches)")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--p", type=float, action="append")
+    a = ap.parse_args()
+    for c in a.configs:
+        run(c, a.shots, a.p, a.reps)
+
+
+if __name__ == "__main__":
+    main()
