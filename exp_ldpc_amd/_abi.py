@@ -67,6 +67,8 @@ SIGNATURES = {
     "qd_osd_last_error": (C.c_char_p, []),
     "qd_graph_set_timing": (_i32, [_p, _i32]),
     "qd_graph_read_timing": (_i32, [_p, _p, _p, _i32, C.POINTER(_i32)]),
+    "qd_osd_device_supported": (_i32, [_p]),
+    "qd_osd_batch_device": (_i32, [_p, _i32, _i32, _i64, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
     "qd_gf2_rref": (_i64, [_p, _i64, _i64, _i64, _p, _i32]),
     "qd_gf2_extend_basis": (_i64, [_p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64]),
 }
@@ -109,9 +111,17 @@ def check(rc: int, what: str = "qdec call") -> None:
 
 
 def ptr(a) -> C.c_void_p | None:
-    """Raw pointer of a numpy array or torch tensor (None passes through)."""
+    """Raw pointer of a numpy array or torch tensor (None passes through).  The
+    C ABI takes dense row-major buffers, so a strided view (e.g. a transposed
+    array) is rejected instead of being read in the wrong order."""
     if a is None:
         return None
     if hasattr(a, "data_ptr"):
+        if not a.is_contiguous():
+            raise ValueError("qdec: tensor arguments must be contiguous (call .contiguous())")
         return C.c_void_p(a.data_ptr())
+    if isinstance(a, C.c_void_p) or isinstance(a, int):
+        return C.c_void_p(a) if isinstance(a, int) else a
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("qdec: array arguments must be C-contiguous (np.ascontiguousarray)")
     return a.ctypes.data_as(C.c_void_p)

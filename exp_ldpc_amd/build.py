@@ -19,7 +19,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libqdec_hip.so")
-SOURCES = ["qdec_abi.cpp", "qdec_osd.cpp", "qdec_gf2.cpp", "qdec_bp.hip", "qdec_bp_block.hip", "qdec_sample.hip"]
+SOURCES = ["qdec_abi.cpp", "qdec_osd.cpp", "qdec_gf2.cpp", "qdec_bp.hip", "qdec_bp_block.hip", "qdec_sample.hip", "qdec_osd.hip"]
 HEADERS = [os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.h"))] + ["../../include/qdec.h"]
 ARCH = os.environ.get("QDEC_OFFLOAD_ARCH", "gfx950")
 

@@ -737,6 +737,47 @@ int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double 
     });
 }
 
+int qd_osd_device_supported(const qd_graph* G) {
+    if (!G) return 0;
+    return osd_kernel_supports(G->dg) ? 1 : 0;
+}
+
+int qd_osd_batch_device(qd_graph* G, int32_t method, int32_t order, int64_t B, const uint8_t* syn, int32_t syn_flags,
+                        const void* llr, int32_t llr_precision, const uint8_t* status, const uint8_t* base,
+                        const uint8_t* readout, uint8_t* osd0_out, uint8_t* osdw_out, uint8_t* corr_out, uint8_t* fail,
+                        void* stream) {
+    return guarded([&] {
+        check_graph(G);
+        if (method < 0 || method > 2) throw Fail(-80, "osd method must be 0 (osd0), 1 (osd_e), 2 (osd_cs)");
+        if (method == 1 && order > 20) throw Fail(-81, "osd_e order above 20 is not supported");
+        if (method == 2 && order > 64) throw Fail(-82, "osd_cs order above 64 is not supported on the device");
+        if (B < 0) throw Fail(-8, "negative batch");
+        if (!llr || (!syn && !syn_flags)) throw Fail(-83, "null OSD inputs");
+        if (llr_precision != QD_F32 && llr_precision != QD_F64) throw Fail(-84, "invalid llr precision");
+        if (!osd_kernel_supports(G->dg)) throw Fail(-85, "graph too large for the device OSD (m <= 256, n < 1024)");
+        if (fail && G->dg.k > 256) throw Fail(-86, "fused failure check after OSD supports <= 256 logicals");
+        if (B == 0) return;
+        set_device(G);
+        OsdArgs a{};
+        a.B = B;
+        a.method = method;
+        a.order = order;
+        a.syn_flags = syn_flags;
+        a.llr_f32 = llr_precision == QD_F32 ? 1 : 0;
+        a.syn = syn;
+        a.llr = llr;
+        a.status = status;
+        a.base = base;
+        a.readout = readout;
+        a.osd0_out = osd0_out;
+        a.osdw_out = osdw_out;
+        a.corr_out = corr_out;
+        a.fail = fail;
+        const int rc = launch_osd(G->dg, a, G->num_cus, (hipStream_t)stream);
+        if (rc != 0) throw Fail(-104, std::string("osd launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
 int qd_graph_set_timing(qd_graph* G, int32_t capacity) {
     return guarded([&] {
         check_graph(G);

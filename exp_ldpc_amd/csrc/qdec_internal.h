@@ -115,6 +115,24 @@ struct DecodeArgs {
     hipEvent_t* ev;    // [3] or nullptr
 };
 
+// Arguments of the GPU OSD stage (qdec_osd.hip).  Shots whose status has bit 0
+// (BP converged) set are skipped; outputs of other shots are left untouched.
+struct OsdArgs {
+    int64_t B;
+    int method, order, syn_flags, llr_f32;
+    const uint8_t* syn;      // [B][m] (nullable with syn_flags)
+    const void* llr;         // [B][n] float or double: BP log-probability ratios
+    const uint8_t* status;   // [B] nullable: every shot is post-processed
+    const uint8_t* base;     // [B][n_data] nullable
+    const uint8_t* readout;  // [B][n_data] nullable
+    uint8_t* osd0_out;       // [B][n] nullable
+    uint8_t* osdw_out;       // [B][n] nullable
+    uint8_t* corr_out;       // [B][n_data] nullable: base ^ fold(osdw)
+    uint8_t* fail;           // [B] nullable: any(Lz (readout ^ corr))
+};
+bool osd_kernel_supports(const DevGraph& g);
+int launch_osd(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream_t stream);
+
 inline void record_ev(const DecodeArgs& a, int i, hipStream_t s) {
     if (a.ev) (void)hipEventRecord(a.ev[i], s);
 }

@@ -193,6 +193,28 @@ class Decoder:
             int(stream_id) & 0xFFFFFFFF, int(shot0), int(B), _abi.ptr(syn), _abi.ptr(readout), C.c_void_p(stream)),
             "qd_sample_storage_device")
 
+    # ------------------------------------------------------------ OSD on the device
+    @property
+    def osd_device_supported(self) -> bool:
+        return bool(self._lib.qd_osd_device_supported(self._handle))
+
+    def osd_device(self, B: int, *, llr, method: str = "osd_cs", order: int = 0, syn=None, syn_flags: int = 0,
+                   status=None, base=None, readout=None, osd0=None, osdw=None, corr=None, fail=None,
+                   stream=None) -> None:
+        """Enqueue OSD (qd_osd_batch_device) for the shots whose `status` lacks
+        the BP-converged bit, on device buffers; `llr` is the BP soft output
+        (float32 or float64 tensor)."""
+        from .osd import OSD_METHODS
+        if method not in OSD_METHODS:
+            raise ValueError(f"unknown OSD method {method!r}")
+        if stream is None:
+            stream = _current_stream(self.device)
+        prec = _abi.QD_F32 if str(getattr(llr, "dtype", "")).endswith("float32") else _abi.QD_F64
+        _abi.check(self._lib.qd_osd_batch_device(
+            self._handle, OSD_METHODS[method], int(order), int(B), _abi.ptr(syn), int(syn_flags), _abi.ptr(llr), prec,
+            _abi.ptr(status), _abi.ptr(base), _abi.ptr(readout), _abi.ptr(osd0), _abi.ptr(osdw), _abi.ptr(corr),
+            _abi.ptr(fail), C.c_void_p(stream)), "qd_osd_batch_device")
+
     # ------------------------------------------------------------ timing
     def set_timing(self, capacity: int) -> None:
         """Record HIP events around the BP and SSF kernels of the next

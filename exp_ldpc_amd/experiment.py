@@ -16,7 +16,9 @@ device.  Decoder modes (``--decoder_mode``):
                      (_experiment.py:128-151); the storage experiment's DEM is
                      written by dem.storage_experiment_dem (R = 0 / 1)
 
-OSD runs on the host cores for the shots BP did not converge on (osd.py).
+OSD runs on the GPU for the shots BP did not converge on (Decoder.osd_device,
+csrc/qdec_osd.hip), fused with the fold and the failure check; graphs too large
+for that kernel use the host stage (osd.py).
 Logical failure = any(Lz (readout + correction)) mod 2 as at _experiment.py:209
 (computed in-kernel for device stages).
 """
@@ -90,6 +92,7 @@ class BatchPipeline:
                       ms_scaling=float(o.get("ms_scaling_factor", 0.0)), device=self.device)
         osd_method = o.get("osd_method", "osd_cs")
         osd_order = int(o.get("osd_order", 0))
+        self.osd_method, self.osd_order = osd_method, osd_order
         self.osd_threads = osd_threads
         R, n = self.R, self.n
         lz = self.L if self.L.shape[0] else None
@@ -172,7 +175,10 @@ class BatchPipeline:
                               else torch.float64, device=dev) if need_llr else None
             self.st.decode_device(B, syn=syn, readout=readout, corr=corr, llr=llr, iters=iters, status=status,
                                   fail=fail)
-            if need_llr:
+            if need_llr and self.st.osd_device_supported:
+                self.st.osd_device(B, llr=llr, method=self.osd_method, order=self.osd_order, syn=syn, status=status,
+                                   readout=readout, corr=corr, fail=fail)
+            elif need_llr:
                 idx, ow = self._osd_fix(self.st, self.st_osd, syn, status, llr, B)
                 if idx is not None:
                     fold = np.zeros((idx.size, n), np.uint8)
@@ -190,8 +196,11 @@ class BatchPipeline:
                                   else torch.float64, device=dev)
                 self.fin.decode_device(B, base=c1, readout=readout, corr=corr, llr=llr, status=status, fail=fail,
                                        syn_flags=3)
-                bad = torch.nonzero((status & 1) == 0).flatten()
-                if bad.numel():
+                bad = torch.nonzero((status & 1) == 0).flatten() if not self.fin.osd_device_supported else None
+                if bad is None:
+                    self.fin.osd_device(B, llr=llr, method=self.osd_method, order=self.osd_order, syn_flags=3,
+                                        status=status, base=c1, readout=readout, corr=corr, fail=fail)
+                elif bad.numel():
                     idx = bad.cpu().numpy()
                     v = (readout.index_select(0, bad) ^ c1.index_select(0, bad)).cpu().numpy()
                     s2 = ((self.H @ v.T).T % 2).astype(np.uint8)
@@ -217,8 +226,11 @@ class BatchPipeline:
                 new_acc = torch.empty((B, n), **u8)
                 s_in = raw.contiguous()
                 self.ss.decode_device(B, syn=s_in, base=acc, corr=new_acc, llr=llr, status=st_t, syn_flags=1)
-                bad = torch.nonzero((st_t & 1) == 0).flatten()
-                if bad.numel():
+                bad = torch.nonzero((st_t & 1) == 0).flatten() if not self.ss.osd_device_supported else None
+                if bad is None:
+                    self.ss.osd_device(B, llr=llr, method=self.osd_method, order=self.osd_order, syn=s_in,
+                                       syn_flags=1, status=st_t, base=acc, corr=new_acc)
+                elif bad.numel():
                     a_h = acc.index_select(0, bad).cpu().numpy()
                     s_h = s_in.index_select(0, bad).cpu().numpy() ^ ((self.H @ a_h.T).T % 2).astype(np.uint8)
                     _, ow = self.ss_osd.solve(s_h, llr.index_select(0, bad).double().cpu().numpy())
@@ -228,8 +240,11 @@ class BatchPipeline:
                               device=dev)
             self.fin.decode_device(B, base=acc, readout=readout, corr=corr, llr=llr, iters=iters, status=status,
                                    fail=fail, syn_flags=3)
-            bad = torch.nonzero((status & 1) == 0).flatten()
-            if bad.numel():
+            bad = torch.nonzero((status & 1) == 0).flatten() if not self.fin.osd_device_supported else None
+            if bad is None:
+                self.fin.osd_device(B, llr=llr, method=self.osd_method, order=self.osd_order, syn_flags=3,
+                                    status=status, base=acc, readout=readout, corr=corr, fail=fail)
+            elif bad.numel():
                 idx = bad.cpu().numpy()
                 a_h = acc.index_select(0, bad).cpu().numpy()
                 v = readout.index_select(0, bad).cpu().numpy() ^ a_h

@@ -1,4 +1,8 @@
-"""Ordered-statistics decoding stage (host C++ in libqdec_hip.so, qd_osd_batch).
+"""Ordered-statistics decoding stage, host side (C++ in libqdec_hip.so,
+qd_osd_batch).  The batched pipelines use the GPU version
+(Decoder.osd_device -> qd_osd_batch_device, csrc/qdec_osd.hip, bit-identical)
+whenever the graph fits it (m <= 256, n < 1024); this host stage serves the
+single-shot ldpc-compatible API and larger graphs.
 
 Post-processes the BP soft output of shots BP did not converge on, as ldpc v1's
 ``bposd_decoder`` does (reference call sites python/qldpc/misc/_experiment.py:23,
@@ -16,7 +20,8 @@ import numpy as np
 from . import _abi
 from .decoder import as_csr01
 
-_METHODS = {"osd0": 0, "osd_e": 1, "osd_cs": 2}
+OSD_METHODS = {"osd0": 0, "osd_e": 1, "osd_cs": 2}
+_METHODS = OSD_METHODS
 
 
 class OsdSolver:

@@ -132,6 +132,21 @@ int qd_osd_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* co
                  uint8_t* osdw_out, int32_t nthreads);
 const char* qd_osd_last_error(void);
 
+/* The same OSD on the GPU, on device-resident buffers, enqueued on `stream`
+ * (hipStream_t).  Graph = the BP graph handle (H, fold and logicals).  Shots with
+ * status bit QD_ST_BP_CONVERGED set are skipped (status nullable: all shots).
+ * llr: [B][n] float (QD_F32) or double (QD_F64), the BP .log_prob_ratios; the
+ * syndrome is syn (^ H[:, :n_data] base/readout per syn_flags, as in
+ * qd_decode_batch).  Outputs for processed shots (each nullable): osd0_out,
+ * osdw_out [B][n] (ldpc .osd0_decoding / .osdw_decoding), corr_out = base ^
+ * fold(osdw), fail = any(Lz (readout ^ corr_out)).  Bit-identical to
+ * qd_osd_batch.  Needs m <= 256 and n < 1024 (qd_osd_device_supported). */
+int qd_osd_device_supported(const qd_graph* g);
+int qd_osd_batch_device(qd_graph* g, int32_t method, int32_t order, int64_t B, const uint8_t* syn, int32_t syn_flags,
+                        const void* llr, int32_t llr_precision, const uint8_t* status, const uint8_t* base,
+                        const uint8_t* readout, uint8_t* osd0_out, uint8_t* osdw_out, uint8_t* corr_out, uint8_t* fail,
+                        void* stream);
+
 /* Kernel timing for measurement: with capacity > 0, the next `capacity` decode
  * calls record HIP events on their launch stream immediately before the BP kernel,
  * after it and after the SSF kernel.  qd_graph_read_timing returns the per-call
