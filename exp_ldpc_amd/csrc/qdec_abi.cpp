@@ -349,8 +349,8 @@ void build_tables(qd_graph* G, int m, int n) {
 }
 
 // Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.
-void attach_queue(qd_graph* G, DecodeArgs& a) {
-    if (!a.ssf || a.B <= 0) return;
+void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
+    if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision))) return;
     const DevGraph& g = G->dg;
     if (a.B > G->q_cap) {
         if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
@@ -372,8 +372,8 @@ void attach_queue(qd_graph* G, DecodeArgs& a) {
     a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
 }
 
-void* message_scratch(qd_graph* G, int precision, size_t* bytes) {
-    const size_t need = block_scratch_bytes(G->dg, precision, G->num_cus);
+void* message_scratch(qd_graph* G, int method, int precision, size_t* bytes) {
+    const size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus);
     *bytes = need;
     if (need == 0) return nullptr;
     if (need > G->mws_bytes) {
@@ -644,10 +644,10 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         if (B < 0) throw Fail(-8, "negative batch");
         set_device(G);
         DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
-        attach_queue(G, a);
+        attach_queue(G, a, p->method, p->precision);
         attach_timing(G, a);
         size_t sb = 0;
-        void* scr = message_scratch(G, p->precision, &sb);
+        void* scr = message_scratch(G, p->method, p->precision, &sb);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
     });
@@ -698,10 +698,10 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         DecodeArgs a = make_args(G, p, B, (const uint8_t*)dptr(r_syn), (const uint8_t*)dptr(r_base),
                                  (const uint8_t*)dptr(r_rd), (uint8_t*)dptr(r_x), (uint8_t*)dptr(r_corr), dptr(r_llr),
                                  (int32_t*)dptr(r_it), (uint8_t*)dptr(r_st), (int32_t*)dptr(r_ss), (uint8_t*)dptr(r_fl));
-        attach_queue(G, a);
+        attach_queue(G, a, p->method, p->precision);
         attach_timing(G, a);
         size_t sb = 0;
-        void* scr = message_scratch(G, p->precision, &sb);
+        void* scr = message_scratch(G, p->method, p->precision, &sb);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         auto d2h = [&](void* h, const Reg& r, const char* what) {

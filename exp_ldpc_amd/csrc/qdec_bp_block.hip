@@ -14,6 +14,9 @@
 // path, with generators spread over the workgroup's threads.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "qdec_device.h"
 
 namespace qdec {
@@ -266,18 +269,28 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
 
 // Small-set-flip for queued shots, one workgroup per shot; generator gi is
 // scanned by thread gi % 256.  Same keys as ssf_wave_kernel.
-__global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArgs a) {
+// gstate: when non-null, the shot state (xh, sres, lpar) of workgroup b lives at
+// gstate + b * block_state_stride(g) in HBM instead of LDS (graphs whose state
+// exceeds the LDS budget, e.g. the 1.2*10^5-column spacetime graph of config 5).
+__host__ __device__ inline size_t block_state_stride(const DevGraph& g) {
+    return (block_small_lds(g) + 255) / 256 * 256;
+}
+
+__global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArgs a, unsigned char* gstate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     long long* redl = reinterpret_cast<long long*>(smem);
     int* redi = reinterpret_cast<int*>(smem + 32);
-    uint8_t* xh = smem + kCtrl;       // [n_pad]
+    uint8_t* xh = gstate ? gstate + (size_t)blockIdx.x * block_state_stride(g) : smem + kCtrl;  // [n_pad]
     uint8_t* sres = xh + g.n_pad;     // [m_pad]
     int* lpar = reinterpret_cast<int*>(sres + g.m_pad);  // [k]
     const int tid = threadIdx.x, m = g.m, n = g.n;
     const int count = *a.q_count;
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
     for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
-        const int64_t shot = a.q_idx[slot];
+        // queue entries of the shot-lane kernel carry its BP-converged bit in bit 62
+        const int64_t qv = a.q_idx[slot];
+        const int64_t shot = qv & ((1ll << 62) - 1);
+        const bool bp_conv = (qv >> 62) & 1;
         for (int j = tid; j < n; j += kBlock) xh[j] = a.q_x[(int64_t)slot * n + j];
         int wl = 0;
         for (int i = tid; i < m; i += kBlock) {
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArg
         }
         int sw = block_sum_i32(wl, redi);  // includes a barrier: LDS fills visible
         int steps = 0;
-        while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
+        while (a.ssf && sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
             long long best = LLONG_MIN;
             for (int gi = tid; gi < g.n_gen; gi += kBlock) {
                 const int nlc = g.g_nlc[gi];
@@ -315,7 +328,212 @@ __global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArg
             sw -= gain;
             ++steps;
         }
-        finalize_block(g, a, shot, xh, false, sw == 0, steps, lpar);
+        finalize_block(g, a, shot, xh, bp_conv, sw == 0, steps, lpar);
+    }
+}
+
+// ---------------------------------------------------------------- shot-lane BP
+// Min-sum BP for graphs whose messages do not fit LDS (configs 4 and 5: 10^4 to
+// 1.2*10^5 columns), laid out for coalesced HBM streaming.  Lane l of every wave
+// of a workgroup works on the shot held by slot l; each workgroup owns a
+// contiguous scratch block of messages stored edge-major, slot-minor
+// (v2c[e][64], c2v[e][64]), so a wave reading edge e of its 64 shots touches one
+// contiguous 256-byte (fp32) run and a check pass walks the block sequentially.
+// Graph indices (row_ptr, col_idx, col_ptr, col_edge, priors) are the same for
+// every lane: scalar loads.  The kLaneWaves waves split the checks (check pass,
+// syndrome test) and the variables (variable pass), with a workgroup barrier
+// between passes.  Slots are refilled as soon as their shot finishes (converged
+// or max_iter): a workgroup-aggregated atomic hands out shot indices, so the
+// work per slot is the shot's own iteration count, not the slowest shot of a
+// group of 64.  Per shot-iteration the HBM traffic is the 16*E-byte message
+// model of SURVEY §8(d) plus n + 2m bytes of hard decisions and syndrome bits.
+// Arithmetic is the block kernel's, operation for operation (row minimum via
+// med3/fmin, column prefix then suffix sums, alpha_t of the shot's own
+// iteration).  Finished shots go to the SSF queue (hard decision, residual,
+// converged bit); ssf_block_kernel runs SSF on the unconverged ones (when
+// asked) and finalises every shot.
+constexpr int kLaneWaves = 8;
+constexpr int kLaneU = 4;     // checks / variables per wave step (loads in flight)
+constexpr int kFinPerCu = 8;  // finalize/SSF workgroups per CU when their state is in HBM
+constexpr size_t kLaneHeader = 256;  // scratch header: the shot counter
+
+template <typename T, int DR, int DC>
+__global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, DecodeArgs a, unsigned char* scratch,
+                                                                  size_t group_bytes) {
+    __shared__ unsigned long long bad_w[kLaneWaves];
+    __shared__ long long next_base;
+    // wave index as a scalar: every graph index below is then a scalar load
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int E = g.E, m = g.m, n = g.n;
+    constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
+    unsigned long long* counter = reinterpret_cast<unsigned long long*>(scratch);
+    unsigned char* blk = scratch + kLaneHeader + (size_t)blockIdx.x * group_bytes;
+    T* v2c = reinterpret_cast<T*>(blk) + lane;                        // [E][64]
+    T* c2v = v2c + (size_t)E * 64;                                    // [E][64]
+    uint8_t* sbit = reinterpret_cast<uint8_t*>(reinterpret_cast<T*>(blk) + (size_t)2 * E * 64) + lane;  // [m][64]
+    uint8_t* xh = sbit + (size_t)m * 64;                              // [n][64]
+    const T* prior = reinterpret_cast<const T*>(g.prior[1][PREC]);
+    const int32_t* rp = g.row_ptr;
+    const int32_t* ci = g.col_idx;
+    const int32_t* cp = g.col_ptr;
+    const int32_t* ce = g.col_edge;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.q_count = (int32_t)a.B;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int64_t shot = -1;   // identical in every wave (all decisions below are workgroup-uniform per lane)
+    int it = 0;
+    bool need = true;
+    for (;;) {
+        // ---- refill finished slots with the next shots
+        const unsigned long long want = __ballot(need);
+        if (want) {
+            if (threadIdx.x == 0) next_base = (long long)atomicAdd(counter, (unsigned long long)__popcll(want));
+            __syncthreads();
+            if (need) {
+                const long long s2 = next_base + __popcll(want & below);
+                shot = s2 < a.B ? s2 : -1;
+                it = 0;
+                if (shot >= 0) {
+                    for (int i = wv; i < m; i += kLaneWaves) {
+                        int s = a.syn ? (a.syn[shot * m + i] & 1) : 0;
+                        if (a.syn_flags)
+                            for (int e = rp[i]; e < rp[i + 1]; ++e) {
+                                const int j = ci[e];
+                                if (j >= g.n_data) continue;
+                                if ((a.syn_flags & 1) && a.base) s ^= a.base[shot * g.n_data + j] & 1;
+                                if ((a.syn_flags & 2) && a.readout) s ^= a.readout[shot * g.n_data + j] & 1;
+                            }
+                        sbit[(size_t)i * 64] = (uint8_t)s;
+                    }
+                    for (int j = wv; j < n; j += kLaneWaves) {
+                        const T pj = prior[j];
+                        for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[(size_t)ce[t] * 64] = pj;
+                    }
+                }
+            }
+            need = false;
+        }
+        const bool active = shot >= 0;
+        if (!__syncthreads_or(active)) break;
+        ++it;
+        const T alpha = alpha_at<T>(it, a.ms_scaling);
+        // Each wave takes kLaneU consecutive checks (or variables) per step and
+        // issues all their loads before using any: kLaneU * DR loads in flight.
+        if (active) {
+            for (int i0 = wv * kLaneU; i0 < m; i0 += kLaneWaves * kLaneU) {  // check pass
+                int e0[kLaneU], d[kLaneU], par[kLaneU];
+                T v[kLaneU][DR];
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) {
+                    const int i = i0 + u;
+                    e0[u] = i < m ? rp[i] : 0;
+                    d[u] = i < m ? rp[i + 1] - e0[u] : 0;
+                    par[u] = i < m ? sbit[(size_t)i * 64] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u)
+#pragma unroll
+                    for (int t = 0; t < DR; ++t)
+                        if (t < d[u]) v[u][t] = v2c[(size_t)(e0[u] + t) * 64];
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) {
+                    T m1 = Big<T>::v, m2 = Big<T>::v;
+                    int pu = par[u];
+#pragma unroll
+                    for (int t = 0; t < DR; ++t)
+                        if (t < d[u]) {
+                            const T av = fabs(v[u][t]);
+                            m2 = med3(av, m1, m2);
+                            m1 = fmin(m1, av);
+                            pu ^= v[u][t] <= (T)0;
+                        }
+                    const T m1a = m1 * alpha, m2a = m2 * alpha;
+#pragma unroll
+                    for (int t = 0; t < DR; ++t)
+                        if (t < d[u]) {
+                            const T y = (fabs(v[u][t]) == m1) ? m2a : m1a;
+                            c2v[(size_t)(e0[u] + t) * 64] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
+                        }
+                }
+            }
+        }
+        __syncthreads();
+        if (active) {
+            for (int j0 = wv * kLaneU; j0 < n; j0 += kLaneWaves * kLaneU) {  // variable pass
+                int t0[kLaneU], d[kLaneU];
+                T c[kLaneU][DC];
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) {
+                    const int j = j0 + u;
+                    t0[u] = j < n ? cp[j] : 0;
+                    d[u] = j < n ? cp[j + 1] - t0[u] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u)
+#pragma unroll
+                    for (int t = 0; t < DC; ++t)
+                        if (t < d[u]) c[u][t] = c2v[(size_t)ce[t0[u] + t] * 64];
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) {
+                    const int j = j0 + u;
+                    if (j >= n) continue;
+                    T pre[DC];
+                    T acc = prior[j];
+#pragma unroll
+                    for (int t = 0; t < DC; ++t)
+                        if (t < d[u]) {
+                            pre[t] = acc;
+                            acc += c[u][t];
+                        }
+                    xh[(size_t)j * 64] = acc <= (T)0;
+                    if (a.llr_out) reinterpret_cast<T*>(a.llr_out)[shot * n + j] = acc;
+                    T suf = (T)0;
+#pragma unroll
+                    for (int t = DC - 1; t >= 0; --t)
+                        if (t < d[u]) {
+                            v2c[(size_t)ce[t0[u] + t] * 64] = pre[t] + suf;
+                            suf += c[u][t];
+                        }
+                }
+            }
+        }
+        __syncthreads();
+        bool bad = false;
+        if (active)
+            for (int i0 = wv * kLaneU; i0 < m; i0 += kLaneWaves * kLaneU) {  // syndrome test
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) {
+                    const int i = i0 + u;
+                    if (i >= m) break;
+                    int par = sbit[(size_t)i * 64];
+                    const int e0 = rp[i], d = rp[i + 1] - e0;
+#pragma unroll
+                    for (int t = 0; t < DR; ++t)
+                        if (t < d) par ^= xh[(size_t)ci[e0 + t] * 64];
+                    bad |= par != 0;
+                }
+            }
+        const unsigned long long bw = __ballot(bad);
+        if (lane == 0) bad_w[wv] = bw;
+        __syncthreads();
+        unsigned long long any = 0;
+#pragma unroll
+        for (int w = 0; w < kLaneWaves; ++w) any |= bad_w[w];
+        const bool conv = active && !((any >> lane) & 1);
+        const bool done = conv || (active && it >= a.max_iter);
+        if (done) {  // queue the shot: hard decision, residual syndrome, converged bit
+            for (int j = wv; j < n; j += kLaneWaves) a.q_x[shot * n + j] = xh[(size_t)j * 64];
+            for (int i = wv; i < m; i += kLaneWaves) {
+                int par = sbit[(size_t)i * 64];
+                for (int e = rp[i]; e < rp[i + 1]; ++e) par ^= xh[(size_t)ci[e] * 64];
+                a.q_r[shot * m + i] = (uint8_t)par;
+            }
+            if (wv == 0) {
+                a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
+                if (a.iters) a.iters[shot] = it;
+            }
+        }
+        need = done;
+        __syncthreads();  // queue reads of sbit/xh and bad_w reads before the refill
     }
 }
 
@@ -337,15 +555,16 @@ static int launch_block(K kern, size_t lds, int64_t work, int num_cus, hipStream
 
 template <typename K>
 static int launch_block2(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
-                         const DecodeArgs& a) {
+                         const DecodeArgs& a, unsigned char* gstate = nullptr, int max_per_cu = 0) {
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
     long long grid = (long long)num_cus * per_cu;
     if (grid > work) grid = work;
     if (grid <= 0) return 0;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, stream, g, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, stream, g, a, gstate);
     return (int)hipGetLastError();
 }
 
@@ -399,7 +618,68 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     return rc;
 }
 
-size_t block_scratch_bytes(const DevGraph& g, int precision, int num_cus) {
+// ---------------------------------------------------------------- shot-lane launch
+template <typename T, int DR, int DC>
+static int launch_lane_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, void* scratch,
+                             size_t scratch_bytes) {
+    const size_t group_bytes = (64 * lane_slot_bytes(g, sizeof(T)) + 255) / 256 * 256;
+    // tail of the scratch: HBM shot state of the finalize/SSF workgroups when it
+    // does not fit LDS (kFinPerCu workgroups per CU)
+    const bool fin_hbm = block_placement(g, sizeof(T)) == 0;
+    const size_t fin_bytes = fin_hbm ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
+    if (scratch_bytes <= fin_bytes + kLaneHeader) return (int)hipErrorOutOfMemory;
+    unsigned char* base = static_cast<unsigned char*>(scratch);
+    unsigned char* fin_state = fin_hbm ? base + (scratch_bytes - fin_bytes) : nullptr;
+    const int64_t max_groups = (int64_t)((scratch_bytes - fin_bytes - kLaneHeader) / group_bytes);
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_lane_kernel<T, DR, DC>, 64 * kLaneWaves, 0);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    int64_t grid = std::min<int64_t>((int64_t)num_cus * per_cu, max_groups);
+    grid = std::min<int64_t>(grid, (a.B + 63) / 64);
+    if (grid <= 0) return (int)hipErrorOutOfMemory;
+    e = hipMemsetAsync(base, 0, sizeof(unsigned long long), stream);  // shot counter
+    if (e != hipSuccess) return (int)e;
+    record_ev(a, 0, stream);
+    hipLaunchKernelGGL((bp_lane_kernel<T, DR, DC>), dim3((unsigned)grid), dim3(64 * kLaneWaves), 0, stream, g, a,
+                       base, group_bytes);
+    hipError_t le = hipGetLastError();
+    record_ev(a, 1, stream);
+    if (le != hipSuccess) return (int)le;
+    const int rc = fin_hbm ? launch_block2(ssf_block_kernel, kCtrl, a.B, num_cus, stream, g, a, fin_state, kFinPerCu)
+                           : launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus,
+                                           stream, g, a);
+    record_ev(a, 2, stream);
+    return rc;
+}
+
+size_t lane_slot_bytes(const DevGraph& g, size_t tsz) {
+    return (size_t)2 * g.E * tsz + (size_t)g.m + (size_t)g.n;
+}
+
+bool lane_kernel_applies(const DevGraph& g, int method, int precision) {
+    if (method != 1 || g.max_rdeg > 16 || g.max_cdeg > 8) return false;
+    const char* opt = getenv("QDEC_LANE_KERNEL");  // opt-in
+    if (!opt || opt[0] != '1') return false;
+    // wherever the workgroup kernel would stream its messages through HBM
+    return block_placement(g, precision == 1 ? 4 : 8) != 3;
+}
+
+static size_t lane_scratch_budget() {
+    const char* v = getenv("QDEC_LANE_SCRATCH_MB");
+    const long long mb = v ? atoll(v) : 24576;  // 24 GiB of the 288 GB HBM
+    return (size_t)std::max(64ll, mb) << 20;
+}
+
+size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus) {
+    if (lane_kernel_applies(g, method, precision)) {
+        const size_t tsz = precision == 1 ? 4 : 8;
+        const size_t per_group = (64 * lane_slot_bytes(g, tsz) + 255) / 256 * 256;
+        const size_t groups = std::max<size_t>(1, std::min<size_t>(lane_scratch_budget() / per_group,
+                                                                   (size_t)num_cus * 8));
+        const size_t fin = block_placement(g, tsz) == 0 ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
+        return kLaneHeader + groups * per_group + fin;
+    }
     const size_t tsz = precision == 1 ? 4 : 8;
     const int placement = block_placement(g, tsz);
     if (placement == 3) return 0;
@@ -410,6 +690,19 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
                         hipStream_t stream, void* scratch, size_t scratch_bytes) {
     if (a.B <= 0) return 0;
     if (a.ssf && g.n_gen <= 0) return (int)hipErrorInvalidValue;
+    if (lane_kernel_applies(g, method, precision)) {
+        if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r || !scratch) return (int)hipErrorInvalidValue;
+        const bool r8 = g.max_rdeg <= 8, c4 = g.max_cdeg <= 4;
+        if (precision == 1)
+            return r8 ? (c4 ? launch_lane_typed<float, 8, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
+                            : launch_lane_typed<float, 8, 8>(g, a, num_cus, stream, scratch, scratch_bytes))
+                      : (c4 ? launch_lane_typed<float, 16, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
+                            : launch_lane_typed<float, 16, 8>(g, a, num_cus, stream, scratch, scratch_bytes));
+        return r8 ? (c4 ? launch_lane_typed<double, 8, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
+                        : launch_lane_typed<double, 8, 8>(g, a, num_cus, stream, scratch, scratch_bytes))
+                  : (c4 ? launch_lane_typed<double, 16, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
+                        : launch_lane_typed<double, 16, 8>(g, a, num_cus, stream, scratch, scratch_bytes));
+    }
     if (precision == 1)
         return method == 1 ? launch_block_typed<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_block_typed<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);

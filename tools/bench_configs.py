@@ -50,7 +50,7 @@ def build_config(name):
     raise SystemExit(f"unknown config {name}")
 
 
-def run(name, shots, ps_override, reps):
+def run(name, shots, ps_override, reps, batch=None):
     import torch
     import scipy.sparse as sp
     from exp_ldpc_amd.decoder import Decoder
@@ -61,7 +61,7 @@ def run(name, shots, ps_override, reps):
     R = cfg["rounds"]
     H = sp.csr_matrix(SpacetimeCode(hz, R).spacetime_check_matrix) if R else hz
     shots = min(shots, cfg.get("max_shots", shots))
-    B = min(cfg["batch"], shots)
+    B = min(batch or cfg["batch"], shots)
     nb = max(1, shots // B)
     dev = torch.device("cuda", 0)
     for p in (ps_override or cfg["ps"]):
@@ -86,8 +86,10 @@ def run(name, shots, ps_override, reps):
         torch.cuda.synchronize()
         dec.set_timing(nb * reps)
         t0 = time.perf_counter()
-        for _ in range(reps):
+        for r in range(reps):
             one_pass()
+            torch.cuda.synchronize()
+            print(f"[{name} p={p}] pass {r + 1}/{reps} {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         bp_ms, ssf_ms = dec.read_timing()
@@ -105,6 +107,7 @@ def run(name, shots, ps_override, reps):
             "ler": float(fail.to(torch.float64).mean().item()) if want_fail else None,
             "bp_kernel_ms_per_launch": float(bp_ms.mean()), "ssf_kernel_ms_per_launch": float(ssf_ms.mean()),
             "E": E, "algorithmic_GBps_bp_kernel": bytes_per_pass / kernel_s / 1e9,
+            "lane_kernel": os.environ.get("QDEC_LANE_KERNEL", "0") == "1",
         }
         print(json.dumps(res), flush=True)
         del syn, rd
@@ -117,9 +120,10 @@ def main():
     ap.add_argument("--shots", type=int, default=1 << 20, help="distinct shots per p (rounded to batches)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--p", type=float, action="append")
+    ap.add_argument("--batch", type=int, default=None, help="shots per launch (default: per config)")
     a = ap.parse_args()
     for c in a.configs:
-        run(c, a.shots, a.p, a.reps)
+        run(c, a.shots, a.p, a.reps, a.batch)
 
 
 if __name__ == "__main__":
