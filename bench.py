@@ -13,6 +13,11 @@ shots are sharded by index (rank r decodes shot range r*B..), no data-path
 collective; a barrier + synchronize brackets the timed region and rank 0 reports
 the max time over ranks.  value = shots decoded by all ranks / that time.
 
+The 9 sweep points are spread round-robin over --streams HIP streams (default
+5), so a point's SSF kernel (latency-bound, few waves) and another point's BP
+kernel (VALU-bound) overlap; kernel durations are then measured under that
+overlap (`--streams 1` gives isolated kernel times).
+
 Also reported: `roofline` for the BP kernel (algorithmic bytes per launch per
 SURVEY §8(d): 334 B/shot of I/O + 16*E B per BP iteration, over the BP kernel's
 average launch duration measured with HIP events the library records on the
@@ -105,6 +110,7 @@ def main():
     ap.add_argument("--p", type=float, action="append", help="decode only these p values (diagnostics)")
     ap.add_argument("--cpu-shots", type=int, default=200000, help="CPU-baseline shots per sweep point")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=5, help="HIP streams the sweep points are spread over")
     args = ap.parse_args()
 
     import torch
@@ -149,12 +155,25 @@ def main():
     ssf_steps = torch.empty((nsteps, len(ps), B), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
-    stream = torch.cuda.current_stream(dev)
+    # sweep points round-robin over HIP streams, so one point's SSF kernel (few,
+    # latency-bound waves) overlaps the next point's BP kernel (VALU-bound); each
+    # point has its own decoder handle, hence its own queue and timing events
+    main = torch.cuda.current_stream(dev)
+    streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
 
     def step(s):
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for st in streams[1:]:
+            st.wait_event(ev)
         for pi in range(len(ps)):
+            st = streams[pi % len(streams)]
             decs[pi].decode_device(B, syn=syn[s, pi], readout=rd[s, pi], iters=iters[s, pi], status=status[s, pi],
-                                   fail=fail[s, pi], ssf_steps=ssf_steps[s, pi], stream=stream.cuda_stream)
+                                   fail=fail[s, pi], ssf_steps=ssf_steps[s, pi], stream=st.cuda_stream)
+        for st in streams[1:]:
+            e2 = torch.cuda.Event()
+            e2.record(st)
+            main.wait_event(e2)
 
     for s in range(args.warmup):
         step(s)
@@ -227,7 +246,7 @@ def main():
                                    "p-sweep geomspace(1e-3,1e-1,9), BP min-sum fp32 max_iter=50 alpha_t=1-2^-t + SSF "
                                    "(Hx flip sets) + fused logical check",
                        "shots_per_point_per_step_per_gpu": B, "global_batch": B * len(ps) * world,
-                       "parallelism": f"shot-sharded x{world}, no collective"},
+                       "parallelism": f"shot-sharded x{world}, no collective", "streams": args.streams},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "bp_ms_wave_kernel<float, 2, 4, 7, true, true, 2> (BP min-sum, fp32, lean outputs, queues BP failures)",

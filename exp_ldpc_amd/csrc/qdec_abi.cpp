@@ -282,8 +282,11 @@ void build_tables(qd_graph* G, int m, int n) {
         for (int i = 0; i < m; ++i)
             for (int e = rp[i]; e < rp[i + 1]; ++e) col_edge[f2[ci[e]]++] = e;
     }
+    std::vector<int32_t> edge_csc(std::max(E, 1), 0);
+    for (int e = 0; e < E; ++e) edge_csc[e] = G->col_ptr[ci[e]] + edge_cpos[e];
     g.col_ptr = G->arena.upload(G->col_ptr);
     g.col_edge = G->arena.upload(col_edge);
+    g.edge_csc = G->arena.upload(edge_csc);
     g.row_ptr = G->arena.upload(G->row_ptr);
     g.col_idx = G->arena.upload(G->col_idx);
     int rc = 0, rv = 0, drc = 0;

@@ -338,7 +338,9 @@ __global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArg
 // of a workgroup works on the shot held by slot l; each workgroup owns a
 // contiguous scratch block of messages stored edge-major, slot-minor
 // (v2c[e][64], c2v[e][64]), so a wave reading edge e of its 64 shots touches one
-// contiguous 256-byte (fp32) run and a check pass walks the block sequentially.
+// contiguous 256-byte (fp32) run.  v2c is kept in CSR (row) order and c2v in
+// CSC (column) order, so both passes read their input sequentially and only
+// their writes scatter (writes do not stall the wave).
 // Graph indices (row_ptr, col_idx, col_ptr, col_edge, priors) are the same for
 // every lane: scalar loads.  The kLaneWaves waves split the checks (check pass,
 // syndrome test) and the variables (variable pass), with a workgroup barrier
@@ -369,7 +371,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
     unsigned long long* counter = reinterpret_cast<unsigned long long*>(scratch);
     unsigned char* blk = scratch + kLaneHeader + (size_t)blockIdx.x * group_bytes;
     T* v2c = reinterpret_cast<T*>(blk) + lane;                        // [E][64]
-    T* c2v = v2c + (size_t)E * 64;                                    // [E][64]
+    T* c2v = v2c + (size_t)E * 64;                                    // [E][64], CSC edge order
     uint8_t* sbit = reinterpret_cast<uint8_t*>(reinterpret_cast<T*>(blk) + (size_t)2 * E * 64) + lane;  // [m][64]
     uint8_t* xh = sbit + (size_t)m * 64;                              // [n][64]
     const T* prior = reinterpret_cast<const T*>(g.prior[1][PREC]);
@@ -377,6 +379,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
     const int32_t* ci = g.col_idx;
     const int32_t* cp = g.col_ptr;
     const int32_t* ce = g.col_edge;
+    const int32_t* ecs = g.edge_csc;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.q_count = (int32_t)a.B;
     const unsigned long long below = (1ull << lane) - 1ull;
     int64_t shot = -1;   // identical in every wave (all decisions below are workgroup-uniform per lane)
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                     for (int t = 0; t < DR; ++t)
                         if (t < d[u]) {
                             const T y = (fabs(v[u][t]) == m1) ? m2a : m1a;
-                            c2v[(size_t)(e0[u] + t) * 64] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
+                            c2v[(size_t)ecs[e0[u] + t] * 64] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
                         }
                 }
             }
@@ -471,7 +474,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                 for (int u = 0; u < kLaneU; ++u)
 #pragma unroll
                     for (int t = 0; t < DC; ++t)
-                        if (t < d[u]) c[u][t] = c2v[(size_t)ce[t0[u] + t] * 64];
+                        if (t < d[u]) c[u][t] = c2v[(size_t)(t0[u] + t) * 64];  // CSC order: contiguous
 #pragma unroll
                 for (int u = 0; u < kLaneU; ++u) {
                     const int j = j0 + u;

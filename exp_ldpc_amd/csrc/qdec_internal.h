@@ -61,6 +61,7 @@ struct DevGraph {
     const int32_t* col_idx;
     const int32_t* col_ptr;       // [n+1]
     const int32_t* col_edge;      // [E] CSR edge ids of column j, ascending row
+    const int32_t* edge_csc;      // [E] CSC position (col_ptr[col] + rank in column) of CSR edge e
     // min-sum wave kernel with compressed check state (qdec_bp_ms.h).  Variables
     // sit in lane slots sorted by degree (ms_vslot); slot edge k scatters its v2c
     // message to element (etab & 0xffff) and gathers check state (etab >> 16);
