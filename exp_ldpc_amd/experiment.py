@@ -407,13 +407,30 @@ def _device_count() -> int:
         return 1
 
 
+def _load_checkpoint(path):
+    """Rows of a previous run's checkpoint CSV, keyed by p (empty when absent)."""
+    import pandas as pd
+    if not path or not os.path.exists(path) or os.path.getsize(path) == 0:
+        return {}
+    df = pd.read_csv(path)
+    return {float(r["p_ph"]): r.to_dict() for _, r in df.iterrows()}
+
+
 def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_prior, *, gpus: int | None = None,
-            seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f32", **kwargs):
+            seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f32", checkpoint: str | None = None,
+            **kwargs):
     """Sweep the physical error rate (reference p_sweep, misc/p_sweep.py:17-40).
     Shots are sharded over `gpus` devices by index (device d decodes a
-    contiguous shot range); exactly `samples` shots per point."""
+    contiguous shot range); exactly `samples` shots per point.
+
+    checkpoint: CSV path; each finished point is appended to it at once, and a
+    restarted sweep reuses the rows already there for the same p, seed and
+    sample count (shots are a pure function of (seed, point index, shot index),
+    so a recomputed point would be identical).  The reference writes its CSV
+    only at the end (misc/p_sweep.py:78)."""
     import pandas as pd
     torch = _torch()
+    done = _load_checkpoint(checkpoint)
     ndev = gpus or _device_count()
     code = kwargs["code"]
     rounds = kwargs["rounds"]
@@ -422,6 +439,10 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
     x_steps, z_steps = _steps(code.checks)
     data = []
     for pi, p_ph in enumerate(p_values):
+        prev = done.get(float(p_ph))
+        if prev is not None and int(prev.get("samples", -1)) == samples and int(prev.get("seed", -1)) == seed:
+            data.append(prev)
+            continue
         t0 = time.perf_counter()
         nm = noise_model(**noise_model_args(p_ph))
         sim = build_storage_simulation(rounds, nm, code, use_x_logicals=False)
@@ -452,7 +473,12 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
                  "ssf_steps_mean": ssf / samples if samples else 0.0}
         del point["code"]
         del point["bp_osd_options"]
+        point["seed"] = seed
         data.append(point)
+        if checkpoint:
+            row = pd.DataFrame.from_records([point])
+            new_file = not os.path.exists(checkpoint) or os.path.getsize(checkpoint) == 0
+            row.to_csv(checkpoint, mode="a", header=new_file, index=False)
     return pd.DataFrame.from_records(data)
 
 
@@ -473,8 +499,8 @@ def parse_sweep_spec(x: str) -> Tuple[float, float, int]:
 
 def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
     """CLI of the sweep (reference p_sweep_main, misc/p_sweep.py:57-78); extra
-    flags: --gpus, --seed, --batch, --precision; extra decoder modes bpssf,
-    bpssf_hybrid, bp."""
+    flags: --gpus, --seed, --batch, --precision, --checkpoint; extra decoder
+    modes bpssf, bpssf_hybrid, bp."""
     parser = ArgumentParser(description="Perform a parallelized sweep in the physical error rate for the given "
                                         "quantum code under BP+OSD / BP+SSF on MI355X")
     parser.add_argument("code", type=Path)
@@ -493,6 +519,8 @@ def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
     parser.add_argument("--seed", type=int, default=DEFAULT_SEED, help="sampler seed (counter-based Philox)")
     parser.add_argument("--batch", type=int, default=1 << 18, help="shots per device launch")
     parser.add_argument("--precision", choices=["f32", "f64"], default="f32", help="BP message precision")
+    parser.add_argument("--checkpoint", type=str, default=None,
+                        help="CSV that each finished point is appended to; finished points are skipped on restart")
     args = parser.parse_args(sys.argv[1:])
     code = load_code(args)
     bp_osd_options = unpack_bposd_args(args, code)
@@ -500,6 +528,7 @@ def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
     result = p_sweep(samples=args.samples, code=code, rounds=args.rounds, noise_model=noise_model,
                      noise_model_args=noise_model_args, meas_prior=meas_prior, data_prior=data_prior,
                      p_values=sweep, decoder_mode=args.decoder_mode, bp_osd_options=bp_osd_options,
-                     gpus=args.gpus, seed=args.seed, batch=args.batch, precision=args.precision)
+                     gpus=args.gpus, seed=args.seed, batch=args.batch, precision=args.precision,
+                     checkpoint=args.checkpoint)
     result.to_csv(sys.stdout)
     return result

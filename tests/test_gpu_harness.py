@@ -222,3 +222,26 @@ def test_bpd_detector_mode_matches_oracle(gpu_available, oracle_lib, rounds):
     for b in range(4):
         corrected = w.readout_correction(np.concatenate([syn_h[b], obs[b]]))
         assert bool(corrected.any()) == bool(ref_fail[b])
+
+
+def test_p_sweep_checkpoint_resume(gpu_available, tmp_path):
+    """--checkpoint: finished points are appended as they complete and reused
+    on restart (same p, seed, samples); new points are computed."""
+    from exp_ldpc_amd.experiment import p_sweep
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    code = load_code("hgp_12_3_4_s1234")
+    opts = {"max_iter": 30, "bp_method": "ms", "ms_scaling_factor": 0, "osd_method": "osd0", "osd_order": 0}
+    prior = lambda p, _, __: 2 * p / 3
+    ck = str(tmp_path / "sweep.csv")
+    kw = dict(samples=4000, noise_model=depolarizing_noise, noise_model_args=lambda p: dict(p=p, pm=p),
+              meas_prior=prior, data_prior=prior, code=code, rounds=0, decoder_mode="bpssf", bp_osd_options=opts,
+              gpus=1, seed=5, batch=2048, checkpoint=ck)
+    first = p_sweep(p_values=[0.01, 0.02], **kw)
+    import pandas as pd
+    assert len(pd.read_csv(ck)) == 2
+    second = p_sweep(p_values=[0.01, 0.02, 0.03], **kw)
+    assert len(pd.read_csv(ck)) == 3
+    assert list(second["failures"][:2]) == list(first["failures"])
+    assert list(second["walltime"][:2]) == list(first["walltime"])  # reused, not recomputed
+    fresh = p_sweep(p_values=[0.03], **{**kw, "checkpoint": None})
+    assert int(second["failures"][2]) == int(fresh["failures"][0])
