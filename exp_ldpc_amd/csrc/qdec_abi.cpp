@@ -353,7 +353,7 @@ void build_tables(qd_graph* G, int m, int n) {
 
 // Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.
 void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
-    if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision))) return;
+    if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision, a.B, G->num_cus))) return;
     const DevGraph& g = G->dg;
     if (a.B > G->q_cap) {
         if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
@@ -375,8 +375,8 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
     a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
 }
 
-void* message_scratch(qd_graph* G, int method, int precision, size_t* bytes) {
-    const size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus);
+void* message_scratch(qd_graph* G, int method, int precision, int64_t B, size_t* bytes) {
+    const size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus, B);
     *bytes = need;
     if (need == 0) return nullptr;
     if (need > G->mws_bytes) {
@@ -650,7 +650,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         attach_queue(G, a, p->method, p->precision);
         attach_timing(G, a);
         size_t sb = 0;
-        void* scr = message_scratch(G, p->method, p->precision, &sb);
+        void* scr = message_scratch(G, p->method, p->precision, B, &sb);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
     });
@@ -704,7 +704,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         attach_queue(G, a, p->method, p->precision);
         attach_timing(G, a);
         size_t sb = 0;
-        void* scr = message_scratch(G, p->method, p->precision, &sb);
+        void* scr = message_scratch(G, p->method, p->precision, B, &sb);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         auto d2h = [&](void* h, const Reg& r, const char* what) {

@@ -360,26 +360,28 @@ constexpr int kFinPerCu = 8;  // finalize/SSF workgroups per CU when their state
 constexpr size_t kLaneHeader = 256;  // scratch header: the shot counter
 
 template <typename T, int DR, int DC>
+// The graph index arrays come in as separate __restrict__ arguments: with no
+// possible aliasing store the compiler can keep their (wave-uniform) loads on the
+// scalar unit (s_load) instead of issuing one vector load per lane.
 __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, DecodeArgs a, unsigned char* scratch,
-                                                                  size_t group_bytes) {
+                                                                  size_t group_bytes,
+                                                                  const int32_t* __restrict__ rp,
+                                                                  const int32_t* __restrict__ ci,
+                                                                  const int32_t* __restrict__ cp,
+                                                                  const int32_t* __restrict__ ce,
+                                                                  const int32_t* __restrict__ ecs,
+                                                                  const T* __restrict__ prior) {
     __shared__ unsigned long long bad_w[kLaneWaves];
     __shared__ long long next_base;
     // wave index as a scalar: every graph index below is then a scalar load
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int E = g.E, m = g.m, n = g.n;
-    constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
     unsigned long long* counter = reinterpret_cast<unsigned long long*>(scratch);
     unsigned char* blk = scratch + kLaneHeader + (size_t)blockIdx.x * group_bytes;
     T* v2c = reinterpret_cast<T*>(blk) + lane;                        // [E][64]
     T* c2v = v2c + (size_t)E * 64;                                    // [E][64], CSC edge order
     uint8_t* sbit = reinterpret_cast<uint8_t*>(reinterpret_cast<T*>(blk) + (size_t)2 * E * 64) + lane;  // [m][64]
     uint8_t* xh = sbit + (size_t)m * 64;                              // [n][64]
-    const T* prior = reinterpret_cast<const T*>(g.prior[1][PREC]);
-    const int32_t* rp = g.row_ptr;
-    const int32_t* ci = g.col_idx;
-    const int32_t* cp = g.col_ptr;
-    const int32_t* ce = g.col_edge;
-    const int32_t* ecs = g.edge_csc;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.q_count = (int32_t)a.B;
     const unsigned long long below = (1ull << lane) - 1ull;
     int64_t shot = -1;   // identical in every wave (all decisions below are workgroup-uniform per lane)
@@ -645,7 +647,8 @@ static int launch_lane_typed(const DevGraph& g, const DecodeArgs& a, int num_cus
     if (e != hipSuccess) return (int)e;
     record_ev(a, 0, stream);
     hipLaunchKernelGGL((bp_lane_kernel<T, DR, DC>), dim3((unsigned)grid), dim3(64 * kLaneWaves), 0, stream, g, a,
-                       base, group_bytes);
+                       base, group_bytes, g.row_ptr, g.col_idx, g.col_ptr, g.col_edge, g.edge_csc,
+                       reinterpret_cast<const T*>(g.prior[1][sizeof(T) == 4 ? 1 : 0]));
     hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;
@@ -660,12 +663,25 @@ size_t lane_slot_bytes(const DevGraph& g, size_t tsz) {
     return (size_t)2 * g.E * tsz + (size_t)g.m + (size_t)g.n;
 }
 
-bool lane_kernel_applies(const DevGraph& g, int method, int precision) {
+// Workgroups of the lane kernel in flight (its occupancy is 2 per CU: 8 waves of
+// <= 128 VGPRs), capped by the HBM scratch budget.
+static size_t lane_groups(const DevGraph& g, size_t tsz, int num_cus);
+
+// Shot-lane kernel or workgroup kernel for a min-sum graph whose messages
+// spill to HBM.  QDEC_LANE_KERNEL=1 forces the lane kernel, =0 the workgroup
+// kernel; by default the lane kernel runs when the per-shot state fits LDS (the
+// finalize stays in LDS) and the batch gives every slot >= 4 shots, so one slow
+// shot does not hold its 63 lane-mates for long.
+bool lane_kernel_applies(const DevGraph& g, int method, int precision, int64_t B, int num_cus) {
     if (method != 1 || g.max_rdeg > 16 || g.max_cdeg > 8) return false;
-    const char* opt = getenv("QDEC_LANE_KERNEL");  // opt-in
-    if (!opt || opt[0] != '1') return false;
-    // wherever the workgroup kernel would stream its messages through HBM
-    return block_placement(g, precision == 1 ? 4 : 8) != 3;
+    const size_t tsz = precision == 1 ? 4 : 8;
+    const int placement = block_placement(g, tsz);
+    if (placement == 3) return false;
+    const char* opt = getenv("QDEC_LANE_KERNEL");
+    if (opt && opt[0] == '1') return true;
+    if (opt && opt[0] == '0') return false;
+    if (placement != 2) return false;
+    return B >= 4 * 64 * (int64_t)lane_groups(g, tsz, num_cus);
 }
 
 static size_t lane_scratch_budget() {
@@ -674,14 +690,17 @@ static size_t lane_scratch_budget() {
     return (size_t)std::max(64ll, mb) << 20;
 }
 
-size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus) {
-    if (lane_kernel_applies(g, method, precision)) {
+static size_t lane_groups(const DevGraph& g, size_t tsz, int num_cus) {
+    const size_t per_group = (64 * lane_slot_bytes(g, tsz) + 255) / 256 * 256;
+    return std::max<size_t>(1, std::min<size_t>(lane_scratch_budget() / per_group, (size_t)num_cus * 2));
+}
+
+size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, int64_t B) {
+    if (lane_kernel_applies(g, method, precision, B, num_cus)) {
         const size_t tsz = precision == 1 ? 4 : 8;
         const size_t per_group = (64 * lane_slot_bytes(g, tsz) + 255) / 256 * 256;
-        const size_t groups = std::max<size_t>(1, std::min<size_t>(lane_scratch_budget() / per_group,
-                                                                   (size_t)num_cus * 8));
         const size_t fin = block_placement(g, tsz) == 0 ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
-        return kLaneHeader + groups * per_group + fin;
+        return kLaneHeader + lane_groups(g, tsz, num_cus) * per_group + fin;
     }
     const size_t tsz = precision == 1 ? 4 : 8;
     const int placement = block_placement(g, tsz);
@@ -693,7 +712,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
                         hipStream_t stream, void* scratch, size_t scratch_bytes) {
     if (a.B <= 0) return 0;
     if (a.ssf && g.n_gen <= 0) return (int)hipErrorInvalidValue;
-    if (lane_kernel_applies(g, method, precision)) {
+    if (lane_kernel_applies(g, method, precision, a.B, num_cus)) {
         if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r || !scratch) return (int)hipErrorInvalidValue;
         const bool r8 = g.max_rdeg <= 8, c4 = g.max_cdeg <= 4;
         if (precision == 1)

@@ -144,8 +144,8 @@ int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs
 int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
                         hipStream_t stream, void* scratch, size_t scratch_bytes);
 int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream);
-size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus);
-bool lane_kernel_applies(const DevGraph& g, int method, int precision);
+size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, int64_t B);
+bool lane_kernel_applies(const DevGraph& g, int method, int precision, int64_t B, int num_cus);
 size_t lane_slot_bytes(const DevGraph& g, size_t tsz);
 int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,
                           uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,

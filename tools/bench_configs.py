@@ -40,7 +40,7 @@ def build_config(name):
         from conftest import load_checks
         hx, hz = load_checks("hgp_80_3_4_s2025")
         _, lz = gf2.css_logicals(hx, hz)
-        return dict(hz=hz, hx=hx, lz=lz, rounds=0, batch=1 << 15, max_shots=1 << 18, ps=[0.01, 0.03],
+        return dict(hz=hz, hx=hx, lz=lz, rounds=0, batch=1 << 17, max_shots=1 << 18, ps=[0.01, 0.03],
                     desc="biregular_hgp(80,3,4,seed=2025) n=10000, R=0, BP ms fp32 max_iter 50 + SSF")
     if name == "c5":
         from exp_ldpc_amd.lifted import psl2_lifted_product_code
