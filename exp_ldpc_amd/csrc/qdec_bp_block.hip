@@ -407,11 +407,11 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                                 if ((a.syn_flags & 1) && a.base) s ^= a.base[shot * g.n_data + j] & 1;
                                 if ((a.syn_flags & 2) && a.readout) s ^= a.readout[shot * g.n_data + j] & 1;
                             }
-                        sbit[(size_t)i * 64] = (uint8_t)s;
+                        sbit[(uint32_t)i * 64u] = (uint8_t)s;
                     }
                     for (int j = wv; j < n; j += kLaneWaves) {
                         const T pj = prior[j];
-                        for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[(size_t)ce[t] * 64] = pj;
+                        for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[(uint32_t)ce[t] * 64u] = pj;
                     }
                 }
             }
@@ -423,7 +423,9 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
         const T alpha = alpha_at<T>(it, a.ms_scaling);
         // Each wave takes kLaneU consecutive checks (or variables) per step and
         // issues all their loads before using any: kLaneU * DR loads in flight.
-        if (active) {
+        // Every lane runs the passes, idle ones on their own (unused) slot, so the
+        // control flow below is wave-uniform: scalar branches, no exec masking.
+        {
             for (int i0 = wv * kLaneU; i0 < m; i0 += kLaneWaves * kLaneU) {  // check pass
                 int e0[kLaneU], d[kLaneU], par[kLaneU];
                 T v[kLaneU][DR];
@@ -432,13 +434,13 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                     const int i = i0 + u;
                     e0[u] = i < m ? rp[i] : 0;
                     d[u] = i < m ? rp[i + 1] - e0[u] : 0;
-                    par[u] = i < m ? sbit[(size_t)i * 64] : 0;
+                    par[u] = i < m ? sbit[(uint32_t)i * 64u] : 0;
                 }
 #pragma unroll
                 for (int u = 0; u < kLaneU; ++u)
 #pragma unroll
                     for (int t = 0; t < DR; ++t)
-                        if (t < d[u]) v[u][t] = v2c[(size_t)(e0[u] + t) * 64];
+                        if (t < d[u]) v[u][t] = v2c[(uint32_t)(e0[u] + t) * 64u];
 #pragma unroll
                 for (int u = 0; u < kLaneU; ++u) {
                     T m1 = Big<T>::v, m2 = Big<T>::v;
@@ -456,13 +458,13 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                     for (int t = 0; t < DR; ++t)
                         if (t < d[u]) {
                             const T y = (fabs(v[u][t]) == m1) ? m2a : m1a;
-                            c2v[(size_t)ecs[e0[u] + t] * 64] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
+                            c2v[(uint32_t)ecs[e0[u] + t] * 64u] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
                         }
                 }
             }
         }
         __syncthreads();
-        if (active) {
+        {
             for (int j0 = wv * kLaneU; j0 < n; j0 += kLaneWaves * kLaneU) {  // variable pass
                 int t0[kLaneU], d[kLaneU];
                 T c[kLaneU][DC];
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                 for (int u = 0; u < kLaneU; ++u)
 #pragma unroll
                     for (int t = 0; t < DC; ++t)
-                        if (t < d[u]) c[u][t] = c2v[(size_t)(t0[u] + t) * 64];  // CSC order: contiguous
+                        if (t < d[u]) c[u][t] = c2v[(uint32_t)(t0[u] + t) * 64u];  // CSC order: contiguous
 #pragma unroll
                 for (int u = 0; u < kLaneU; ++u) {
                     const int j = j0 + u;
@@ -489,13 +491,13 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                             pre[t] = acc;
                             acc += c[u][t];
                         }
-                    xh[(size_t)j * 64] = acc <= (T)0;
-                    if (a.llr_out) reinterpret_cast<T*>(a.llr_out)[shot * n + j] = acc;
+                    xh[(uint32_t)j * 64u] = acc <= (T)0;
+                    if (a.llr_out && active) reinterpret_cast<T*>(a.llr_out)[shot * n + j] = acc;
                     T suf = (T)0;
 #pragma unroll
                     for (int t = DC - 1; t >= 0; --t)
                         if (t < d[u]) {
-                            v2c[(size_t)ce[t0[u] + t] * 64] = pre[t] + suf;
+                            v2c[(uint32_t)ce[t0[u] + t] * 64u] = pre[t] + suf;
                             suf += c[u][t];
                         }
                 }
@@ -503,21 +505,22 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
         }
         __syncthreads();
         bool bad = false;
-        if (active)
+        {
             for (int i0 = wv * kLaneU; i0 < m; i0 += kLaneWaves * kLaneU) {  // syndrome test
 #pragma unroll
                 for (int u = 0; u < kLaneU; ++u) {
                     const int i = i0 + u;
                     if (i >= m) break;
-                    int par = sbit[(size_t)i * 64];
+                    int par = sbit[(uint32_t)i * 64u];
                     const int e0 = rp[i], d = rp[i + 1] - e0;
 #pragma unroll
                     for (int t = 0; t < DR; ++t)
-                        if (t < d) par ^= xh[(size_t)ci[e0 + t] * 64];
+                        if (t < d) par ^= xh[(uint32_t)ci[e0 + t] * 64u];
                     bad |= par != 0;
                 }
             }
-        const unsigned long long bw = __ballot(bad);
+        }
+        const unsigned long long bw = __ballot(bad && active);
         if (lane == 0) bad_w[wv] = bw;
         __syncthreads();
         unsigned long long any = 0;
@@ -526,10 +529,10 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
         const bool conv = active && !((any >> lane) & 1);
         const bool done = conv || (active && it >= a.max_iter);
         if (done) {  // queue the shot: hard decision, residual syndrome, converged bit
-            for (int j = wv; j < n; j += kLaneWaves) a.q_x[shot * n + j] = xh[(size_t)j * 64];
+            for (int j = wv; j < n; j += kLaneWaves) a.q_x[shot * n + j] = xh[(uint32_t)j * 64u];
             for (int i = wv; i < m; i += kLaneWaves) {
-                int par = sbit[(size_t)i * 64];
-                for (int e = rp[i]; e < rp[i + 1]; ++e) par ^= xh[(size_t)ci[e] * 64];
+                int par = sbit[(uint32_t)i * 64u];
+                for (int e = rp[i]; e < rp[i + 1]; ++e) par ^= xh[(uint32_t)ci[e] * 64u];
                 a.q_r[shot * m + i] = (uint8_t)par;
             }
             if (wv == 0) {
