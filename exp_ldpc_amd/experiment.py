@@ -412,7 +412,7 @@ def _load_checkpoint(path):
     import pandas as pd
     if not path or not os.path.exists(path) or os.path.getsize(path) == 0:
         return {}
-    df = pd.read_csv(path)
+    df = pd.read_csv(path, float_precision="round_trip")
     return {float(r["p_ph"]): r.to_dict() for _, r in df.iterrows()}
 
 
@@ -478,7 +478,7 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
         if checkpoint:
             row = pd.DataFrame.from_records([point])
             new_file = not os.path.exists(checkpoint) or os.path.getsize(checkpoint) == 0
-            row.to_csv(checkpoint, mode="a", header=new_file, index=False)
+            row.to_csv(checkpoint, mode="a", header=new_file, index=False, float_format="%.17g")
     return pd.DataFrame.from_records(data)
 
 

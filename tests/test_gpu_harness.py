@@ -242,6 +242,6 @@ def test_p_sweep_checkpoint_resume(gpu_available, tmp_path):
     second = p_sweep(p_values=[0.01, 0.02, 0.03], **kw)
     assert len(pd.read_csv(ck)) == 3
     assert list(second["failures"][:2]) == list(first["failures"])
-    assert list(second["walltime"][:2]) == list(first["walltime"])  # reused, not recomputed
-    fresh = p_sweep(p_values=[0.03], **{**kw, "checkpoint": None})
-    assert int(second["failures"][2]) == int(fresh["failures"][0])
+    assert np.allclose(second["walltime"][:2], first["walltime"], rtol=1e-9, atol=0)  # reused, not recomputed
+    fresh = p_sweep(p_values=[0.01, 0.02, 0.03], **{**kw, "checkpoint": None})  # same point indices (streams)
+    assert list(second["failures"]) == list(fresh["failures"])
