@@ -451,20 +451,31 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
         pipes = [BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision, noise=nm)
                  for d in range(ndev)]
         per = math.ceil(samples / ndev)
-        failures = conv = iters = ssf = 0
-        for d, pipe in enumerate(pipes):
+
+        def shard(d):
+            """Device d's contiguous shot range; returns its counters."""
+            pipe = pipes[d]
             lo, hi = d * per, min(samples, (d + 1) * per)
+            acc = [0, 0, 0, 0]
             with torch.cuda.device(d):
                 for start in range(lo, hi, batch):
                     b = min(batch, hi - start)
                     syn, rd = sim.sample_device(pipe.sampler_graph, b, seed, pi, start)
                     res = pipe.run(syn, rd)
-                    failures += int(res.fail.sum())
-                    conv += res.bp_converged
-                    iters += res.iters_sum
-                    ssf += res.ssf_steps_sum
-        for d in range(ndev):
-            torch.cuda.synchronize(d)
+                    acc[0] += int(res.fail.sum())
+                    acc[1] += res.bp_converged
+                    acc[2] += res.iters_sum
+                    acc[3] += res.ssf_steps_sum
+                torch.cuda.synchronize(d)
+            return acc
+
+        if ndev == 1:
+            parts = [shard(0)]
+        else:  # one host thread per device: each pipeline blocks on its own D2H copies
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=ndev) as ex:
+                parts = list(ex.map(shard, range(ndev)))
+        failures, conv, iters, ssf = (sum(p[i] for p in parts) for i in range(4))
         runtime = time.perf_counter() - t0
         point = {"p_ph": p_ph, "failures": failures, "samples": samples, "walltime": runtime, **kwargs,
                  **bp_osd_options, "gpus": ndev, "shots_per_s": samples / runtime if runtime > 0 else float("nan"),
