@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--cpu-shots", type=int, default=200000, help="CPU-baseline shots per sweep point")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=5, help="HIP streams the sweep points are spread over")
+    ap.add_argument("--heavy-first", action="store_true", help="launch the sweep points from the highest p down")
     args = ap.parse_args()
 
     import torch
@@ -161,13 +162,15 @@ def main():
     main = torch.cuda.current_stream(dev)
     streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
 
+    order = list(range(len(ps)))[::-1] if args.heavy_first else list(range(len(ps)))
+
     def step(s):
         ev = torch.cuda.Event()
         ev.record(main)
         for st in streams[1:]:
             st.wait_event(ev)
-        for pi in range(len(ps)):
-            st = streams[pi % len(streams)]
+        for li, pi in enumerate(order):
+            st = streams[li % len(streams)]
             decs[pi].decode_device(B, syn=syn[s, pi], readout=rd[s, pi], iters=iters[s, pi], status=status[s, pi],
                                    fail=fail[s, pi], ssf_steps=ssf_steps[s, pi], stream=st.cuda_stream)
         for st in streams[1:]:

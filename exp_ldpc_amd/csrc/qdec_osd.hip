@@ -16,14 +16,17 @@
 //      candidate keeping a tie.
 //
 // One wave64 per shot (persistent over the batch).  Row i of the augmented
-// matrix [H_sorted | s] lives in registers of lane i % 64, slot i / 64 (RS slots,
-// W 64-bit words), so a pivot step is: a ballot per slot to find the pivot, two
+// matrix [H_sorted | s] lives in registers of lane i % 64, slot i / 64 (RS <= 6
+// slots: m <= 384, i.e. spacetime graphs up to R = 2; W <= 16 64-bit words:
+// n < 1024), so a pivot step is: a ballot per slot to find the pivot, two
 // readlanes per word to broadcast the pivot row, and one masked XOR per word and
 // slot -- no LDS traffic inside the elimination.  The sort is a bitonic network
 // in LDS on (order-preserving key, column) pairs.  Candidate scoring reads the
 // reduced matrix back from LDS: a transformed column is RS ballots, its weight
 // RS scalar popcounts.  The fused fold + logical check reuses finalize_shot.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "qdec_device.h"
 #include "qdec_internal.h"
@@ -72,20 +75,31 @@ __device__ __forceinline__ uint64_t order_key(double v) {
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
+// Calls f(std::integral_constant<int, I>) for I = B .. E-1 (compile-time indices).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// Bit k of a W-word register row.  Written as masked arithmetic over every word:
+// an `if (w == k >> 6)` select chain is folded back by the compiler into a
+// dynamically indexed array, which demotes the whole row to scratch memory.
 template <int W>
 __device__ __forceinline__ void flip_bit(uint64_t (&r)[W], int k) {
+    const uint64_t bit = 1ull << (k & 63);
 #pragma unroll
-    for (int w = 0; w < W; ++w)
-        if (w == (k >> 6)) r[w] ^= 1ull << (k & 63);
+    for (int w = 0; w < W; ++w) r[w] ^= bit & (0ull - (uint64_t)((unsigned)(k - 64 * w) < 64u));
 }
 
 template <int W>
 __device__ __forceinline__ int get_bit(const uint64_t (&r)[W], int k) {
-    int v = 0;
+    uint64_t v = 0;
 #pragma unroll
-    for (int w = 0; w < W; ++w)
-        if (w == (k >> 6)) v = (int)((r[w] >> (k & 63)) & 1);
-    return v;
+    for (int w = 0; w < W; ++w) v |= r[w] & (0ull - (uint64_t)((unsigned)(k - 64 * w) < 64u));
+    return (int)((v >> (k & 63)) & 1);
 }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -179,13 +193,16 @@ __global__ __launch_bounds__(64) void osd_wave_kernel(DevGraph g, OsdArgs a) {
             }
         }
 
-        // ---- 3. Gauss-Jordan in sorted column order
+        // ---- 3. Gauss-Jordan in sorted column order.  The word index is a
+        // compile-time constant in every instantiation of `step` (static_for), so
+        // row[][] stays in registers (a runtime word index would demote it to
+        // scratch memory).
         int rank = 0;
-#pragma unroll
-        for (int ww = 0; ww < W; ++ww) {
+        static_for<0, W>([&](auto wwc) {
+            constexpr int ww = decltype(wwc)::value;
             for (int b = 0; b < 64; ++b) {
                 const int k = ww * 64 + b;
-                if (k >= n || rank >= m) break;
+                if (k >= n || rank >= m) return;
                 int piv = -1;
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
@@ -234,7 +251,7 @@ __global__ __launch_bounds__(64) void osd_wave_kernel(DevGraph g, OsdArgs a) {
                 }
                 ++rank;
             }
-        }
+        });
 
         // ---- 4. reduced rows to LDS, transformed syndrome, non-pivot columns
         uint64_t x0[RS];
@@ -402,11 +419,13 @@ int launch_osd_shape(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream
 }
 }  // namespace
 
-#define QDEC_OSD_SHAPES(X) X(2, 4) X(2, 6) X(2, 9) X(2, 16) X(4, 6) X(4, 9) X(4, 12) X(4, 16)
+#define QDEC_OSD_SHAPES(X) X(2, 4) X(2, 6) X(2, 9) X(2, 16) X(4, 6) X(4, 9) X(4, 12) X(4, 16) X(6, 14) X(6, 16)
+
+static int osd_row_slots(int m) { return m <= 128 ? 2 : (m <= 256 ? 4 : 6); }
 
 bool osd_kernel_supports(const DevGraph& g) {
-    if (g.m <= 0 || g.m > 256 || g.n + 1 > 1024) return false;
-    const int rs = g.m <= 128 ? 2 : 4;
+    if (g.m <= 0 || g.m > 384 || g.n + 1 > 1024) return false;
+    const int rs = osd_row_slots(g.m);
     const int need = (g.n + 1 + 63) / 64;
 #define QDEC_OSD_FITS(R, V) if (rs == R && need <= V) return true;
     QDEC_OSD_SHAPES(QDEC_OSD_FITS)
@@ -417,7 +436,7 @@ bool osd_kernel_supports(const DevGraph& g) {
 int launch_osd(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream_t stream) {
     if (a.B <= 0) return 0;
     if (!osd_kernel_supports(g)) return (int)hipErrorNotSupported;
-    const int rs = g.m <= 128 ? 2 : 4;
+    const int rs = osd_row_slots(g.m);
     const int need = (g.n + 1 + 63) / 64;
 #define QDEC_OSD_LAUNCH(R, V) \
     if (rs == R && need <= V) return launch_osd_shape<R, V>(g, a, num_cus, stream);

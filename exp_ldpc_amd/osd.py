@@ -1,7 +1,7 @@
 """Ordered-statistics decoding stage, host side (C++ in libqdec_hip.so,
 qd_osd_batch).  The batched pipelines use the GPU version
 (Decoder.osd_device -> qd_osd_batch_device, csrc/qdec_osd.hip, bit-identical)
-whenever the graph fits it (m <= 256, n < 1024); this host stage serves the
+whenever the graph fits it (m <= 384, n < 1024); this host stage serves the
 single-shot ldpc-compatible API and larger graphs.
 
 Post-processes the BP soft output of shots BP did not converge on, as ldpc v1's

@@ -140,7 +140,7 @@ const char* qd_osd_last_error(void);
  * qd_decode_batch).  Outputs for processed shots (each nullable): osd0_out,
  * osdw_out [B][n] (ldpc .osd0_decoding / .osdw_decoding), corr_out = base ^
  * fold(osdw), fail = any(Lz (readout ^ corr_out)).  Bit-identical to
- * qd_osd_batch.  Needs m <= 256 and n < 1024 (qd_osd_device_supported). */
+ * qd_osd_batch.  Needs m <= 384 and n < 1024 (qd_osd_device_supported). */
 int qd_osd_device_supported(const qd_graph* g);
 int qd_osd_batch_device(qd_graph* g, int32_t method, int32_t order, int64_t B, const uint8_t* syn, int32_t syn_flags,
                         const void* llr, int32_t llr_precision, const uint8_t* status, const uint8_t* base,

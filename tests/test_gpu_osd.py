@@ -25,6 +25,7 @@ def _graphs():
     return {
         "R0": sp.csr_matrix(HZ),
         "R1": sp.csr_matrix(SpacetimeCode(HZ, 1).spacetime_check_matrix),
+        "R2": sp.csr_matrix(SpacetimeCode(HZ, 2).spacetime_check_matrix),
         "single_shot": sp.csr_matrix(SpacetimeCodeSingleShot(HZ).spacetime_check_matrix),
         "ragged": make_check_matrix(rows, n),
     }
