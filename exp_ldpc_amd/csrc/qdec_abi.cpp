@@ -487,6 +487,8 @@ int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t*
             G->dg.k = 0;
             G->dg.lz = nullptr;
             G->dg.n_gen = 0;
+            G->dg.g_inv = nullptr;
+            G->dg.g_invd = G->dg.g_invl = 0;
         } catch (...) {
             G->arena.release();
             if (G->stream) (void)hipStreamDestroy(G->stream);
@@ -530,6 +532,7 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         for (int gi = 0; gi < gp; ++gi)
             for (int c = 0; c < kGenLC; ++c) lc8[(size_t)(c / 4) * gp + gi] |= (uint32_t)g.m_pad << (8 * (c % 4));
         int wmax = 0, nlcmax = 0;
+        std::vector<std::vector<uint16_t>> inv(g.m_pad);  // check -> (generator, local bit)
         for (int gi = 0; gi < n_gen; ++gi) {
             const int a = gen_ptr[gi], b = gen_ptr[gi + 1];
             if (b < a) throw Fail(-31, "gen_ptr not monotone");
@@ -551,6 +554,7 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
             nlcmax = std::max(nlcmax, (int)checks.size());
             for (size_t c = 0; c < checks.size(); ++c) {
                 lc[c * gp + gi] = (uint16_t)checks[c];
+                if (gi < 256) inv[checks[c]].push_back((uint16_t)(gi | (c << 8)));
                 uint32_t& word = lc8[(c / 4) * gp + gi];
                 word = (word & ~(0xffu << (8 * (c % 4)))) | ((uint32_t)checks[c] << (8 * (c % 4)));
             }
@@ -565,8 +569,22 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
                 qm[(size_t)k * gp + gi] = mask;
             }
         }
+        size_t invmax = 1;
+        for (const auto& v : inv) invmax = std::max(invmax, v.size());
+        int invl = 0;
+        while ((size_t)1 << invl < invmax) ++invl;
+        const int invd = 1 << invl;
+        std::vector<uint16_t> invt;
+        if (pack8 && n_gen <= 128 && invd <= 64) {
+            invt.assign((size_t)g.m_pad * invd, 0xffff);
+            for (int i = 0; i < g.m_pad; ++i)
+                for (size_t t = 0; t < inv[i].size(); ++t) invt[(size_t)i * invd + t] = inv[i][t];
+        }
         G->flip_arena.release();
         g.g_lc8 = nullptr;
+        g.g_inv = invt.empty() ? nullptr : G->flip_arena.upload(invt);
+        g.g_invd = invt.empty() ? 0 : invd;
+        g.g_invl = invt.empty() ? 0 : invl;
         g.g_w = G->flip_arena.upload(w);
         g.g_nlc = G->flip_arena.upload(nlc);
         g.g_q = G->flip_arena.upload(q);

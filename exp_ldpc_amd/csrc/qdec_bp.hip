@@ -310,11 +310,17 @@ struct SsfLds {
     static constexpr int GP = 64 * RG;
     static constexpr int kStage = 3;  // packed queue entries staged per wave (two slots ahead)
     __host__ __device__ static size_t table_bytes() { return (size_t)GP * 4 * (kGenW + kGenLC / 4 + kGenW / 2); }
-    __host__ __device__ static size_t shared_bytes(const DevGraph& g) {
-        return table_bytes() + (lz_in_lds(g) ? ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16 : 0);
+    __host__ __device__ static size_t lz_bytes(const DevGraph& g) {
+        return lz_in_lds(g) ? ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16 : 0;
     }
+    __host__ __device__ static size_t inv_bytes(const DevGraph& g) {
+        return g.g_inv ? ((size_t)g.m_pad * g.g_invd * 2 + 15) / 16 * 16 : 0;
+    }
+    __host__ __device__ static size_t shared_bytes(const DevGraph& g) { return table_bytes() + lz_bytes(g) + inv_bytes(g); }
+    // residual, cached keys, listed local syndromes, current local syndromes,
+    // flipped-check list, listed generators, hard decision, staged queue entries
     __host__ __device__ static size_t wave_bytes(const DevGraph& g) {
-        return (((size_t)g.m_pad + 64) * 4 + (size_t)GP * 4 * 2 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16 +
+        return (((size_t)g.m_pad + 64) * 4 + (size_t)GP * 4 * 3 + kGenLC * 4 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16 +
                256 * kStage;
     }
 };
@@ -335,11 +341,15 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint64_t* lzs_lds = reinterpret_cast<uint64_t*>(smem + SsfLds<RG>::table_bytes());
     const uint64_t* lzs = lz_in_lds(g) ? lzs_lds : g.lz;
+    uint16_t* invt = reinterpret_cast<uint16_t*>(smem + SsfLds<RG>::table_bytes() + SsfLds<RG>::lz_bytes(g));
+    const bool inc = g.g_inv != nullptr;  // incremental local syndromes
     unsigned char* wbase = smem + SsfLds<RG>::shared_bytes(g) + (size_t)wave * SsfLds<RG>::wave_bytes(g);
     uint32_t* sres = reinterpret_cast<uint32_t*>(wbase);      // [m_pad + 64] residual (pads stay 0)
     int* key = reinterpret_cast<int*>(sres + g.m_pad + 64);   // [GP] cached best keys
     uint32_t* slt = reinterpret_cast<uint32_t*>(key + GP);    // [GP] local syndromes of listed gens
-    uint8_t* list = reinterpret_cast<uint8_t*>(slt + GP);     // [GP] listed generators
+    uint32_t* slc = slt + GP;                                 // [GP] current local syndromes (inc)
+    uint32_t* clist = slc + GP;                               // [kGenLC] checks flipped by a step (inc)
+    uint8_t* list = reinterpret_cast<uint8_t*>(clist + kGenLC);  // [GP] listed generators
     uint8_t* xh = list + GP;                                  // [n_pad + 64]
     uint8_t* ent = wbase + SsfLds<RG>::wave_bytes(g) - 256 * SsfLds<RG>::kStage;  // [kStage][256] queue entries
     const int m = g.m, n = g.n;
@@ -355,6 +365,8 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
     }
     if (lz_in_lds(g))
         for (int e = threadIdx.x; e < g.k * g.lz_words; e += 64 * kSsfWaves) lzs_lds[e] = g.lz[e];
+    if (inc)
+        for (int e = threadIdx.x; e < g.m_pad * g.g_invd; e += 64 * kSsfWaves) invt[e] = g.g_inv[e];
     for (int e = lane; e < g.m_pad + 64; e += 64) sres[e] = 0;
     for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
     __syncthreads();
@@ -410,19 +422,26 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
         int steps = 0;
         bool first = true;
         while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
-            // ---- 1. local syndromes; compact the changed, non-zero ones ----
+            // ---- 1. local syndromes (gathered from the residual on the first
+            // step, afterwards kept current by step 4); compact the changed,
+            // non-zero ones ----
             int nl = 0;
 #pragma unroll
             for (int rg = 0; rg < RG; ++rg) {
                 const int gi = rg * 64 + lane;
                 uint32_t sl = 0;
+                if (first || !inc) {
 #pragma unroll
-                for (int wq = 0; wq < NLW; ++wq) {
-                    if (wq < nlcw) {
-                        const uint32_t pk = lct[wq * GP + gi];
+                    for (int wq = 0; wq < NLW; ++wq) {
+                        if (wq < nlcw) {
+                            const uint32_t pk = lct[wq * GP + gi];
 #pragma unroll
-                        for (int bb = 0; bb < 4; ++bb) sl |= sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
+                            for (int bb = 0; bb < 4; ++bb) sl |= sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
+                        }
                     }
+                    if (inc) slc[gi] = sl;
+                } else {
+                    sl = slc[gi];
                 }
                 const bool changed = first || sl != slo[rg];
                 slo[rg] = sl;
@@ -496,7 +515,19 @@ __global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g,
             const int gain = score * __builtin_popcount(tsel) / kSsfScale;
             if (lane < kGenLC && ((fm >> lane) & 1)) {
                 const uint32_t wv = lct[(lane >> 2) * GP + gsel];
-                sres[(wv >> (8 * (lane & 3))) & 0xff] ^= 1u;
+                const uint32_t c = (wv >> (8 * (lane & 3))) & 0xff;
+                sres[c] ^= 1u;
+                clist[__builtin_popcount(fm & ((1u << lane) - 1u))] = c;
+            }
+            if (inc) {
+                // every generator with a flipped check as local check `bit`
+                // toggles that bit: (check, entry) pairs spread over the lanes
+                wave_lds_sync();
+                const int npair = __builtin_popcount(fm) << g.g_invl;
+                for (int pr = lane; pr < npair; pr += 64) {
+                    const uint32_t e = invt[(clist[pr >> g.g_invl] << g.g_invl) + (pr & (g.g_invd - 1))];
+                    if (e != 0xffffu) atomicXor(&slc[e & 0xff], 1u << (e >> 8));
+                }
             }
             if (lane < kGenW && ((tsel >> lane) & 1)) {
                 const uint32_t qv = qt[(lane >> 1) * GP + gsel];

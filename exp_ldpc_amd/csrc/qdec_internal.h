@@ -81,6 +81,12 @@ struct DevGraph {
     const uint16_t* g_lc;         // [kGenLC][g_pad]  local check c of generator g
     const uint32_t* g_lc8;        // [kGenLC/4][g_pad] the same ids packed 4 per word (pad -> m_pad)
     int g_nlcmax;
+    // inverse of the local-check lists, for the wave SSF kernel's incremental
+    // local syndromes: [m_pad][g_invd] u16 entries g | (bit << 8) (generator g has
+    // check i as local check `bit`), pad 0xffff; g_invd a power of two (log2:
+    // g_invl).  nullptr when unavailable (the kernel re-gathers every step).
+    const uint16_t* g_inv;
+    int g_invd, g_invl;
     const uint32_t* g_qmask;      // [kGenW][g_pad]   local-check mask of qubit k
     // logicals (fused failure check)
     int k, lz_words;

@@ -1,7 +1,7 @@
 """Dev: phase timers of the min-sum kernel (needs libqdec_hip_stamps.so)."""
 import ctypes as C, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["QDEC_LIB"] = os.path.join(ROOT, "exp_ldpc_amd", "libqdec_hip_stamps.so")
+os.environ.setdefault("QDEC_LIB", os.path.join(ROOT, "exp_ldpc_amd", "libqdec_hip_stamps.so"))
 sys.path.insert(0, ROOT)
 import numpy as np, torch
 from exp_ldpc_amd import _abi
