@@ -575,7 +575,11 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         while ((size_t)1 << invl < invmax) ++invl;
         const int invd = 1 << invl;
         std::vector<uint16_t> invt;
-        if (pack8 && n_gen <= 128 && invd <= 64) {
+        // QDEC_SSF_GATHER=1: no inverse table, the wave SSF kernel re-gathers the
+        // local syndromes every step (the path of graphs whose table is too wide)
+        const char* gather_env = std::getenv("QDEC_SSF_GATHER");
+        const bool gather = gather_env && gather_env[0] == '1';
+        if (pack8 && n_gen <= 128 && invd <= 64 && !gather) {
             invt.assign((size_t)g.m_pad * invd, 0xffff);
             for (int i = 0; i < g.m_pad; ++i)
                 for (size_t t = 0; t < inv[i].size(); ++t) invt[(size_t)i * invd + t] = inv[i][t];

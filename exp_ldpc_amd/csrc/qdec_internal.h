@@ -117,6 +117,10 @@ struct DecodeArgs {
     // check (RW = m_pad/64 words); replaces q_idx/q_x/q_r
     int q_packed;
     uint64_t* q_w;
+    // workgroup BP kernel with HBM message slices: shot counter handing out
+    // shots dynamically (a straggler does not hold up a fixed stride of shots);
+    // nullptr -> static stride.  Set by the launcher.
+    unsigned long long* work_ctr;
     // optional timing (host side only): events recorded on the launch stream
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr

@@ -81,6 +81,16 @@ def test_hgp10k_bp_ssf_parity(gpu_available, oracle_lib, hgp10k):
     assert got["ssf_steps"].sum() > 0
 
 
+def test_hgp10k_lane_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
+    """The opt-in shot-lane HBM-streaming kernel (QDEC_LANE_KERNEL=1) on C4."""
+    monkeypatch.setenv("QDEC_LANE_KERNEL", "1")
+    hx, hz, lz = hgp10k
+    p = 0.03
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=9, shot0=0, B=160)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=30, keys=KEYS_SSF)
+    assert got["ssf_steps"].sum() > 0
+
+
 def test_hgp10k_bp_f64_llr(gpu_available, oracle_lib, hgp10k):
     from test_gpu_parity import _cmp_llr
     from exp_ldpc_amd.decoder import Decoder
@@ -122,11 +132,14 @@ def test_psl13_lift_bp_parity(gpu_available, oracle_lib, psl13_hz):
     _decode_both(oracle_lib, hz, 2 * p / 3, syn, max_iter=15)
 
 
-def test_psl13_lift_spacetime_r1_parity(gpu_available, oracle_lib, psl13_hz):
+@pytest.mark.parametrize("kernel", ["workgroup", "lane"])
+def test_psl13_lift_spacetime_r1_parity(gpu_available, oracle_lib, psl13_hz, kernel, monkeypatch):
     """C5's multi-round spacetime syndromes: H_st = [blockdiag(Hz, Hz) | M]
     (spacetime_code.py:46-75), sampled by the storage-experiment sampler at R = 1
     and folded onto the data qubits."""
     from exp_ldpc_amd.spacetime import SpacetimeCode
+    if kernel == "lane":
+        monkeypatch.setenv("QDEC_LANE_KERNEL", "1")
     hz = psl13_hz
     H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
     p = 0.005

@@ -62,8 +62,14 @@ def test_bp_parity(gpu_available, oracle_lib, method, precision, shape):
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("max_iter", [1, 3, 50])
-def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, code225):
+@pytest.mark.parametrize("local_syndromes", ["incremental", "gather"])
+def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, local_syndromes, code225, monkeypatch):
+    """Both ways the wave SSF kernel keeps generator-local syndromes: updated
+    through the check -> generator table after each flip (default), or
+    re-gathered from the residual every step (QDEC_SSF_GATHER=1)."""
     from exp_ldpc_amd.decoder import Decoder
+    if local_syndromes == "gather":
+        monkeypatch.setenv("QDEC_SSF_GATHER", "1")
     rng = np.random.default_rng(max_iter)
     B = 2000
     rd = _errors(rng, B, 225, 0.03)

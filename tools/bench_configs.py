@@ -45,7 +45,7 @@ def build_config(name):
     if name == "c5":
         from exp_ldpc_amd.lifted import psl2_lifted_product_code
         hz = psl2_lifted_product_code(13).checks.z
-        return dict(hz=sp.csr_matrix(hz), hx=None, lz=None, rounds=1, batch=1 << 11, max_shots=1 << 15, ps=[0.002, 0.005],
+        return dict(hz=sp.csr_matrix(hz), hx=None, lz=None, rounds=1, batch=1 << 15, max_shots=1 << 15, ps=[0.002, 0.005],
                     desc="PSL(2,13) matrix lift n=49140, R=1 spacetime (39312x117936), BP ms fp32 max_iter 50")
     raise SystemExit(f"unknown config {name}")
 
