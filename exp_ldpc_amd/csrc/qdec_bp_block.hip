@@ -142,6 +142,10 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
     const int32_t* ci = g.col_idx;
     const int32_t* cp = g.col_ptr;
     const int32_t* ce = g.col_edge;
+    // the unrolled min-sum instantiation stores c2v in CSC (column) order, so the
+    // column pass reads it sequentially and only the row pass's writes scatter
+    const int32_t* ecs = g.edge_csc;
+    constexpr bool kCsc = METHOD == 1 && DRM > 0;
 
     // next shot: from the launcher's counter (dynamic, a.work_ctr) or by stride
     long long* next_s = reinterpret_cast<long long*>(smem + 56);
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                     for (int t = 0; t < DRM; ++t)
                         if (t < d) {
                             const T y = (fabs(v[t]) == m1) ? m2a : m1a;
-                            c2v[e0 + t] = (par ^ (v[t] <= (T)0)) ? -y : y;
+                            c2v[ecs[e0 + t]] = (par ^ (v[t] <= (T)0)) ? -y : y;
                         }
                 } else if constexpr (METHOD == 1) {
                     T m1 = Big<T>::v, m2 = Big<T>::v;
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                         if (t < d) ev[t] = ce[t0 + t];
 #pragma unroll
                     for (int t = 0; t < DCM; ++t)
-                        if (t < d) c[t] = c2v[ev[t]];
+                        if (t < d) c[t] = c2v[t0 + t];  // CSC order: contiguous
 #pragma unroll
                     for (int t = 0; t < DCM; ++t)
                         if (t < d) {
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                 T acc = prior[j];
                 for (int t = cp[j]; t < cp[j + 1]; ++t) {
                     if constexpr (METHOD == 1) {
-                        acc += c2v[ce[t]];
+                        acc += c2v[kCsc ? t : ce[t]];
                     } else {
                         acc *= c2v[ce[t]];
                         if (isnan(acc)) acc = (T)1;

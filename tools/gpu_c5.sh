@@ -7,5 +7,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_la
 tail -1 $O/tests.log
 timeout -k 10 600 python -u tools/bench_configs.py c5 --reps 2 > $O/c5.jsonl 2> $O/c5.err
 cut -c1-420 $O/c5.jsonl
-QDEC_LANE_KERNEL=0 timeout -k 10 600 python -u tools/bench_configs.py c4 --reps 2 --batch 131072 --shots 262144 > $O/c4_block.jsonl 2> $O/c4_block.err
+timeout -k 10 600 python -u tools/bench_configs.py c4 --reps 2 --batch 131072 --shots 262144 > $O/c4_block.jsonl 2> $O/c4_block.err
 cut -c1-420 $O/c4_block.jsonl
