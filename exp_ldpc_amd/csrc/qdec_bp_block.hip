@@ -146,6 +146,11 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
     // column pass reads it sequentially and only the row pass's writes scatter
     const int32_t* ecs = g.edge_csc;
     constexpr bool kCsc = METHOD == 1 && DRM > 0;
+    // placement 0 (byte arrays in HBM): the unrolled instantiation also keeps the
+    // hard decision as bits in LDS ([n_pad/64] words, one ballot per wave), so the
+    // syndrome test gathers bits from LDS instead of bytes from HBM
+    uint64_t* xbits = reinterpret_cast<uint64_t*>(smem + kCtrl);
+    const bool xb = DRM > 0 && placement == 0;
 
     // next shot: from the launcher's counter (dynamic, a.work_ctr) or by stride
     long long* next_s = reinterpret_cast<long long*>(smem + 56);
@@ -170,8 +175,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
             }
             sb[i] = (uint8_t)s;
         }
-        for (int j = tid; j < n; j += kBlock)
-            for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[ce[t]] = prior[j];
+        for (int e = tid; e < E; e += kBlock) v2c[e] = prior[ci[e]];  // CSR order: coalesced
         __syncthreads();
         int it = 1;
         bool conv = false;
@@ -253,6 +257,10 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                             acc += c[t];
                         }
                     xh[j] = acc <= (T)0;
+                    if (xb) {
+                        const uint64_t w = __ballot(acc <= (T)0);
+                        if ((tid & 63) == 0) xbits[j >> 6] = w;
+                    }
                     T suf = (T)0;
 #pragma unroll
                     for (int t = DCM - 1; t >= 0; --t)
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                         if (t < d) cc[t] = ci[e0 + t];
 #pragma unroll
                     for (int t = 0; t < DRM; ++t)
-                        if (t < d) par ^= xh[cc[t]];
+                        if (t < d) par ^= xb ? (int)((xbits[cc[t] >> 6] >> (cc[t] & 63)) & 1ull) : (int)xh[cc[t]];
                 } else {
                     for (int e = rp[i]; e < rp[i + 1]; ++e) par ^= xh[ci[e]];
                 }
@@ -674,7 +682,8 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
     const size_t msg = ((size_t)2 * g.E * sizeof(T) + 15) / 16 * 16;
     const size_t small = (block_small_lds(g) + 15) / 16 * 16;
     const int placement = block_placement(g, sizeof(T));
-    const size_t lds = (placement & 2) ? small + ((placement & 1) ? msg : 0) : kCtrl;
+    // placement 0: control area + the hard-decision bits of the unrolled kernel
+    const size_t lds = (placement & 2) ? small + ((placement & 1) ? msg : 0) : kCtrl + (size_t)g.n_pad / 8;
     int cap = 0;
     T* gs = nullptr;
     DecodeArgs a = a0;
