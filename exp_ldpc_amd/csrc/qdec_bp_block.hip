@@ -108,7 +108,7 @@ __host__ __device__ inline size_t block_slice_bytes(const DevGraph& g, size_t ts
     return (b + 255) / 256 * 256;
 }
 
-// DRM / DCM > 0 (min-sum, row degree <= DRM, column degree <= DCM): the row and
+// DRM / DCM > 0 (row degree <= DRM, column degree <= DCM; both methods): the row and
 // column loops are unrolled to that width with every load of a row (column)
 // issued before any use, and the column pass keeps its prefix sums in registers
 // (one scattered read and one scattered write per edge instead of five).  Same
@@ -142,10 +142,10 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
     const int32_t* ci = g.col_idx;
     const int32_t* cp = g.col_ptr;
     const int32_t* ce = g.col_edge;
-    // the unrolled min-sum instantiation stores c2v in CSC (column) order, so the
+    // the unrolled instantiations store c2v in CSC (column) order, so the
     // column pass reads it sequentially and only the row pass's writes scatter
     const int32_t* ecs = g.edge_csc;
-    constexpr bool kCsc = METHOD == 1 && DRM > 0;
+    constexpr bool kCsc = DRM > 0;
     // placement 0 (byte arrays in HBM): the unrolled instantiation also keeps the
     // hard decision as bits in LDS ([n_pad/64] words, one ballot per wave), so the
     // syndrome test gathers bits from LDS instead of bytes from HBM
@@ -222,6 +222,29 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                         const T y = (fabs(v) == m1) ? m2a : m1a;
                         c2v[e] = (par ^ (v <= (T)0)) ? -y : y;
                     }
+                } else if constexpr (DRM > 0) {
+                    // product-sum, unrolled: forward products, then backward
+                    const int d = e1 - e0;
+                    T v[DRM], r[DRM], fw[DRM];
+#pragma unroll
+                    for (int t = 0; t < DRM; ++t)
+                        if (t < d) v[t] = v2c[e0 + t];
+                    T f = sb[i] ? (T)-1 : (T)1;
+#pragma unroll
+                    for (int t = 0; t < DRM; ++t)
+                        if (t < d) {
+                            fw[t] = f;
+                            r[t] = (T)2 / ((T)1 + v[t]) - (T)1;
+                            f *= r[t];
+                        }
+                    T b = (T)1;
+#pragma unroll
+                    for (int t = DRM - 1; t >= 0; --t)
+                        if (t < d) {
+                            const T c = fw[t] * b;
+                            c2v[ecs[e0 + t]] = ((T)1 - c) / ((T)1 + c);
+                            b *= r[t];
+                        }
                 } else {
                     T f = sb[i] ? (T)-1 : (T)1;
                     for (int e = e0; e < e1; ++e) {
@@ -281,6 +304,37 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                         v2c[e] = v2c[e] + suf;
                         suf += c2v[e];
                     }
+                } else if constexpr (DCM > 0) {
+                    // product-sum, unrolled (NaN guards as in the generic loop)
+                    const int d = t1 - t0;
+                    int ev[DCM];
+                    T c[DCM], pre[DCM];
+#pragma unroll
+                    for (int t = 0; t < DCM; ++t)
+                        if (t < d) ev[t] = ce[t0 + t];
+#pragma unroll
+                    for (int t = 0; t < DCM; ++t)
+                        if (t < d) c[t] = c2v[t0 + t];  // CSC order: contiguous
+#pragma unroll
+                    for (int t = 0; t < DCM; ++t)
+                        if (t < d) {
+                            pre[t] = acc;
+                            acc *= c[t];
+                            if (isnan(acc)) acc = (T)1;
+                        }
+                    xh[j] = acc >= (T)1;
+                    if (xb) {
+                        const uint64_t w = __ballot(acc >= (T)1);
+                        if ((tid & 63) == 0) xbits[j >> 6] = w;
+                    }
+                    T suf = (T)1;
+#pragma unroll
+                    for (int t = DCM - 1; t >= 0; --t)
+                        if (t < d) {
+                            v2c[ev[t]] = pre[t] * suf;
+                            suf *= c[t];
+                            if (isnan(suf)) suf = (T)1;
+                        }
                 } else {
                     for (int t = t0; t < t1; ++t) {
                         const int e = ce[t];
@@ -332,7 +386,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                     if constexpr (METHOD == 1) {
                         acc += c2v[kCsc ? t : ce[t]];
                     } else {
-                        acc *= c2v[ce[t]];
+                        acc *= c2v[kCsc ? t : ce[t]];
                         if (isnan(acc)) acc = (T)1;
                     }
                 }
@@ -699,9 +753,9 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
         const hipError_t e0 = hipMemsetAsync(a.work_ctr, 0, sizeof(unsigned long long), stream);
         if (e0 != hipSuccess) return (int)e0;
     }
-    // min-sum graphs with row degree <= 16 and column degree <= 8: unrolled loops
-    const bool unr = METHOD == 1 && g.max_rdeg <= 16 && g.max_cdeg <= 8;
-    constexpr int UR = METHOD == 1 ? 16 : 0, UC = METHOD == 1 ? 8 : 0;
+    // graphs with row degree <= 16 and column degree <= 8: unrolled loops
+    const bool unr = g.max_rdeg <= 16 && g.max_cdeg <= 8;
+    constexpr int UR = 16, UC = 8;
     if (!a.ssf) {
         record_ev(a, 0, stream);
         const int rc = unr ? launch_block(bp_block_kernel<T, METHOD, false, UR, UC>, lds, a.B, num_cus, stream, cap, g, a,
