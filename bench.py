@@ -3,27 +3,40 @@
 
 One step = one pass of the hot path over one batch per sweep point: for each
 p in geomspace(1e-3, 1e-1, 9), decode B device-resident storage-experiment shots
-(R = 0: H = Hz 108x225) with BP min-sum (fp32, max_iter 50, alpha_t = 1-2^-t)
+(R = 0: H = Hz 108x225) with BP min-sum (max_iter 50, alpha_t = 1-2^-t)
 + small-set-flip on BP failures + fused logical-failure check.  Inputs for every
 step are sampled on the device *before* the timed region (distinct shots per
 step; on-device Philox sampler), so the timed region is decode only.
 
-Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU;
-shots are sharded by index (rank r decodes shot range r*B..), no data-path
-collective; a barrier + synchronize brackets the timed region and rank 0 reports
-the max time over ranks.  value = shots decoded by all ranks / that time.
+Precision: the headline line (`value`, `dtype`) runs BP in f64, ldpc v1's
+message precision (its loops use double).  The same shots are then decoded in
+f32 (the stated-tolerance variant) and reported under `variants`.
 
-The 9 sweep points are spread round-robin over --streams HIP streams (default
-5), so a point's SSF kernel (latency-bound, few waves) and another point's BP
-kernel (VALU-bound) overlap; kernel durations are then measured under that
-overlap (`--streams 1` gives isolated kernel times).
+Phases (rank 0 prints ONE JSON line):
+  1. headline: W warmup + K timed steps, the 9 points spread over --streams HIP
+     streams (one point's SSF kernel overlaps another point's BP kernel);
+  2. f32 variant: the same shots, same timing protocol;
+  3. isolated launches (--iso-steps, one stream): per-kernel durations from HIP
+     events the library records on the launch stream around each kernel; the
+     roofline uses these (overlapped launches share the chip, so their durations
+     are not one kernel's);
+  4. sampling + decode: K steps with the sampler inside the timed region.
 
-Also reported: `roofline` for the BP kernel (algorithmic bytes per launch per
-SURVEY §8(d): 334 B/shot of I/O + 16*E B per BP iteration, over the BP kernel's
-average launch duration measured with HIP events the library records on the
-launch stream immediately around it; the SSF kernel's time is listed beside), and
-`cpu_baseline`: the CPU oracle (oracle/, a C port of the same algorithm, OpenMP)
-timed on the host cores on a bounded sample of the same workload (rank 0, N=1).
+Multi-GPU: `torchrun --nproc-per-node N bench.py --gpus N` (one process per
+GPU), or `python bench.py --gpus N`, which starts that torchrun as a child
+process before anything touches the GPU and exits with its status.  Shots are
+sharded by index (rank r decodes shot range (step*N + r)*B ..), no data-path
+collective; a barrier + synchronize brackets the timed region and rank 0
+reports the max time over ranks.  value = shots decoded by all ranks / time.
+
+Roofline (dominant kernel = the f64 BP kernel): `achieved` = algorithmic HBM
+bytes per launch (the compulsory per-shot I/O, 339 B: 108 B syndrome + 225 B
+readout in, fail + status + 4-B iteration count out) / the kernel's isolated
+average launch time.  BP messages live in LDS/registers at n = 225 and never
+touch HBM, so this fraction is small by construction; the ceilings that bind
+(VALU issue, LDS) come from the committed PMC summary of this same command
+(profiles/*_pmc_summary.json; tools/pmc.sh + tools/pmc_summary.py), as does
+`traffic` (HBM bytes per launch, FETCH_SIZE x2 + WRITE_SIZE).
 """
 from __future__ import annotations
 
@@ -32,6 +45,8 @@ import glob
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,7 +58,8 @@ sys.path.insert(0, REPO)
 METRIC = "decoded syndrome shots/sec + logical error rate, (3,4)-HGP n=225 @ 1/2/4/8 GPUs"
 CODE = "hgp_12_3_4_s1234"
 SEED = 20250221
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+IO_BYTES_PER_SHOT = 108 + 225 + 1 + 1 + 4  # syndrome + readout in; fail, status, iters out
 
 
 def wilson(k: int, n: int, z: float = 1.96):
@@ -56,48 +72,199 @@ def wilson(k: int, n: int, z: float = 1.96):
     return (max(0.0, c - h), min(1.0, c + h))
 
 
+def overlap(a, b) -> bool:
+    return a[0] <= b[1] and b[0] <= a[1]
+
+
 def load_code():
     from exp_ldpc_amd.codes import read_quantum_code
     with open(os.path.join(REPO, "tests", "golden", f"{CODE}.qecc")) as f:
         return read_quantum_code(f, validate_stabilizer_code=True)
 
 
-def latest_traffic():
-    """Per-launch HBM bytes of the decode kernel from the newest committed PMC
-    summary (profiles/*_pmc_summary.json, written by tools/pmc_summary.py)."""
+def pmc_ceilings(kernel_prefix: str):
+    """Per-launch PMC figures of the BP kernel from the newest committed PMC
+    summary (profiles/*_pmc_summary.json, written by tools/pmc_summary.py from
+    a rocprofv3 --pmc run of this bench command), or None."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            return json.load(f).get("decode_kernel_hbm_bytes_per_launch")
-    except Exception:
-        return None
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except Exception:
+            continue
+        for name, k in d.get("kernels", {}).items():
+            if name.startswith(kernel_prefix) and "derived" in k:
+                return os.path.relpath(f, REPO), name, k
+    return None
 
 
-def cpu_baseline(code, ps, args, gpu_ler):
-    """Time the CPU oracle on a bounded sample of the same workload."""
+def launch_children(args) -> int:
+    """`python bench.py --gpus N` without a launcher: run torchrun with N ranks as
+    a child process (nothing here has touched the GPU) and return its status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_baseline(code, ps, args):
+    """Time the CPU oracle (C port of the same algorithm, f64 like ldpc, OpenMP
+    over shots) on a bounded sample of the same workload; its failure counts
+    give the CPU LER curve the GPU curves are compared with."""
     from oracle import load as load_oracle
     orc = load_oracle()
     hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 64))
     per_p = args.cpu_shots
-    total = 0
     elapsed = 0.0
     fails = {}
     for pi, p in enumerate(ps):
         syn, rd = orc.sample_storage(hz, 0, p, p, seed=SEED, stream=pi, shot0=0, B=per_p, nthreads=threads)
         t0 = time.perf_counter()
-        out = orc.decode(hz, 2 * p / 3, syn, method="ms", precision="f32", max_iter=50, ssf=True, gens=hx, lz=lz,
+        out = orc.decode(hz, 2 * p / 3, syn, method="ms", precision="f64", max_iter=50, ssf=True, gens=hx, lz=lz,
                          readout=rd, want_llr=False, nthreads=threads, ssf_impl="fast")
         elapsed += time.perf_counter() - t0
-        total += per_p
         fails[f"{p:.6g}"] = int(out["fail"].sum())
-    return {"value": total / elapsed, "unit": "shots/s", "cores": threads, "kind": "port",
-            "sample": f"{per_p} shots at each of the {len(ps)} sweep points (same sampler/seed as the GPU run, "
-                      f"shot indices 0..{per_p - 1}); decode only, sampling excluded; {elapsed:.1f} s of CPU work",
-            "failures_per_point": fails}
+    total = per_p * len(ps)
+    return {"value": total / elapsed, "unit": "shots/s", "cores": threads, "kind": "port", "dtype": "f64",
+            "sample": f"{per_p} shots at each of the {len(ps)} sweep points (same sampler and seed as the GPU run, "
+                      f"shot indices 0..{per_p - 1}, i.e. the warmup step's shots, disjoint from the timed ones); "
+                      f"BP min-sum f64 max_iter 50 + SSF + logical check, decode only; {elapsed:.1f} s of CPU work "
+                      f"on {threads} threads",
+            "failures_per_point": fails, "shots_per_point": per_p}
+
+
+class FakeDecoder:
+    """--fake-device (CPU tests of the launcher and the rank merge only): a
+    stand-in with the decode_device signature; shot s fails iff (s + point) is odd."""
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def sample_storage_device(self, rounds, p_data, p_meas, seed, stream_id, shot0, B, syn, readout, stream=None):
+        import torch
+        syn.copy_(((torch.arange(shot0, shot0 + B, device=self.dev)[:, None] + stream_id) % 2).to(torch.uint8))
+        readout.zero_()
+
+    def decode_device(self, B, *, syn=None, readout=None, iters=None, status=None, fail=None, ssf_steps=None,
+                      stream=None, **_):
+        fail.copy_((syn[:, 0] == 1).to(fail.dtype))
+        iters.fill_(1)
+        status.fill_(3)
+        ssf_steps.zero_()
+
+    def set_timing(self, capacity):
+        self.cap = capacity
+
+    def read_timing(self):
+        return np.full(self.cap, 1e-3), np.full(self.cap, 1e-3)
+
+
+class Run:
+    """Device-resident inputs and outputs of every step, and the timed loop."""
+
+    def __init__(self, args, ps, m, n, world, rank, dev, torch, fake):
+        self.args, self.ps, self.torch, self.dev = args, ps, torch, dev
+        self.world, self.rank, self.fake = world, rank, fake
+        self.B = args.batch
+        self.nsteps = args.warmup + args.steps
+        P = len(ps)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        self.syn = torch.empty((self.nsteps, P, self.B, m), **u8)
+        self.rd = torch.empty((self.nsteps, P, self.B, n), **u8)
+        self.iters = torch.empty((self.nsteps, P, self.B), dtype=torch.int32, device=dev)
+        self.status = torch.empty((self.nsteps, P, self.B), **u8)
+        self.fail = torch.empty((self.nsteps, P, self.B), **u8)
+        self.ssf_steps = torch.empty((self.nsteps, P, self.B), dtype=torch.int32, device=dev)
+        if fake:
+            self.streams = [None]
+        else:
+            main = torch.cuda.current_stream(dev)
+            self.streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
+
+    def shot0(self, s):
+        return (s * self.world + self.rank) * self.B
+
+    def sample(self, sampler, s, stream=None):
+        for pi, p in enumerate(self.ps):
+            sampler.sample_storage_device(0, p, p, SEED, pi, self.shot0(s), self.B, self.syn[s, pi], self.rd[s, pi],
+                                          **({} if stream is None else {"stream": stream}))
+
+    def sync(self):
+        if not self.fake:
+            self.torch.cuda.synchronize(self.dev)
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def step(self, decs, s, streams):
+        torch = self.torch
+        if self.fake or len(streams) == 1:
+            for pi in range(len(self.ps)):
+                decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
+                                       status=self.status[s, pi], fail=self.fail[s, pi],
+                                       ssf_steps=self.ssf_steps[s, pi],
+                                       **({} if self.fake else {"stream": streams[0].cuda_stream}))
+            return
+        ev = torch.cuda.Event()
+        ev.record(streams[0])
+        for st in streams[1:]:
+            st.wait_event(ev)
+        for pi in range(len(self.ps)):
+            st = streams[pi % len(streams)]
+            decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
+                                   status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi],
+                                   stream=st.cuda_stream)
+        for st in streams[1:]:
+            e2 = torch.cuda.Event()
+            e2.record(st)
+            streams[0].wait_event(e2)
+
+    def timed(self, decs, steps, streams, sampler=None, warm=True):
+        """Run the warmup steps (untimed, unless warm=False), then `steps` timed
+        steps; returns the max-over-ranks wall time of the timed ones."""
+        a = self.args
+        for s in range(a.warmup if warm else 0):
+            self.step(decs, s, streams)
+        self.sync()
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        for s in range(a.warmup, a.warmup + steps):
+            if sampler is not None:
+                self.sample(sampler, s, None if self.fake else streams[0].cuda_stream)
+            self.step(decs, s, streams)
+        self.sync()
+        self.barrier()
+        elapsed = time.perf_counter() - t0
+        if self.world > 1:
+            import torch.distributed as dist
+            tt = self.torch.tensor([elapsed], dtype=self.torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        return elapsed
+
+    def counts(self):
+        """Failures / BP-converged per point over the timed steps, summed over ranks."""
+        torch = self.torch
+        w = self.args.warmup
+        fails = self.fail[w:].to(torch.int64).sum(dim=(0, 2)).cpu()
+        conv = (self.status[w:] & 1).to(torch.int64).sum(dim=(0, 2)).cpu()
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(fails)
+            dist.all_reduce(conv)
+        itp = self.iters[w:].to(torch.float64).mean(dim=(0, 2)).cpu().numpy()
+        ssp = self.ssf_steps[w:].to(torch.float64).mean(dim=(0, 2)).cpu().numpy()
+        return fails.numpy(), conv.numpy(), itp, ssp
 
 
 def main():
@@ -108,161 +275,183 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 18, help="shots per sweep point per step per GPU")
     ap.add_argument("--points", type=int, default=9)
     ap.add_argument("--p", type=float, action="append", help="decode only these p values (diagnostics)")
+    ap.add_argument("--precision", default="f64", choices=["f32", "f64"], help="headline BP precision")
+    ap.add_argument("--variant", default="f32", choices=["f32", "f64", "none"],
+                    help="second precision decoded on the same shots (reported under variants)")
     ap.add_argument("--cpu-shots", type=int, default=200000, help="CPU-baseline shots per sweep point")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=5, help="HIP streams the sweep points are spread over")
-    ap.add_argument("--heavy-first", action="store_true", help="launch the sweep points from the highest p down")
+    ap.add_argument("--iso-steps", type=int, default=2, help="isolated (one-stream) steps timing each kernel")
+    ap.add_argument("--no-sample-phase", action="store_true", help="skip the sampling+decode phase")
+    ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    args.iso_steps = max(1, min(args.iso_steps, args.steps))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_children(args))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    from exp_ldpc_amd.decoder import Decoder
+    fake = args.fake_device
+    if fake:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
 
     code = load_code()
     hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
     m, n = hz.shape
-    E = int(hz.nnz)
     ps = np.geomspace(1e-3, 1e-1, args.points) if not args.p else np.array(args.p)
-    B = args.batch
-    nsteps = args.warmup + args.steps
+    P = len(ps)
 
-    dec = Decoder(hz, 2 * ps[0] / 3, method="ms", precision="f32", max_iter=50, ms_scaling=0.0,
-                  flip_sets=hx, logicals=lz, device=local)
-    # one decoder graph per sweep point (priors differ), sharing nothing mutable
-    decs = [dec] + [Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, flip_sets=hx, logicals=lz,
-                            device=local) for p in ps[1:]]
+    def decoders(precision):
+        if fake:
+            return [FakeDecoder(dev) for _ in ps]
+        from exp_ldpc_amd.decoder import Decoder
+        # one decoder graph per sweep point (priors differ), sharing nothing mutable
+        return [Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0,
+                        flip_sets=hx, logicals=lz, device=local) for p in ps]
 
-    # ---- inputs: distinct shots for every (step, point), sampled on device ----
-    syn = torch.empty((nsteps, len(ps), B, m), dtype=torch.uint8, device=dev)
-    rd = torch.empty((nsteps, len(ps), B, n), dtype=torch.uint8, device=dev)
-    for s in range(nsteps):
-        for pi, p in enumerate(ps):
-            shot0 = (s * world + rank) * B
-            dec.sample_storage_device(0, p, p, SEED, pi, shot0, B, syn[s, pi], rd[s, pi])
-    iters = torch.empty((nsteps, len(ps), B), dtype=torch.int32, device=dev)
-    status = torch.empty((nsteps, len(ps), B), dtype=torch.uint8, device=dev)
-    fail = torch.empty((nsteps, len(ps), B), dtype=torch.uint8, device=dev)
-    ssf_steps = torch.empty((nsteps, len(ps), B), dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
+    run = Run(args, ps, m, n, world, rank, dev, torch, fake)
+    decs = decoders(args.precision)
+    for s in range(run.nsteps):  # distinct shots for every (step, point), sampled on device
+        run.sample(decs[0], s)
+    run.sync()
 
-    # sweep points round-robin over HIP streams, so one point's SSF kernel (few,
-    # latency-bound waves) overlaps the next point's BP kernel (VALU-bound); each
-    # point has its own decoder handle, hence its own queue and timing events
-    main = torch.cuda.current_stream(dev)
-    streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
+    # ---- phase 1: headline precision, overlapped streams ----
+    elapsed = run.timed(decs, args.steps, run.streams)
+    fails, conv, itp, ssp = run.counts()
+    shots_per_point = args.steps * args.batch * world
+    total_shots = shots_per_point * P
 
-    order = list(range(len(ps)))[::-1] if args.heavy_first else list(range(len(ps)))
+    # ---- phase 2: the other precision on the same shots ----
+    variant = None
+    if args.variant not in ("none", args.precision):
+        vdecs = decoders(args.variant)
+        v_elapsed = run.timed(vdecs, args.steps, run.streams)
+        v_fails, v_conv, _, _ = run.counts()
+        variant = (args.variant, v_elapsed, v_fails, v_conv, vdecs)
 
-    def step(s):
-        ev = torch.cuda.Event()
-        ev.record(main)
-        for st in streams[1:]:
-            st.wait_event(ev)
-        for li, pi in enumerate(order):
-            st = streams[li % len(streams)]
-            decs[pi].decode_device(B, syn=syn[s, pi], readout=rd[s, pi], iters=iters[s, pi], status=status[s, pi],
-                                   fail=fail[s, pi], ssf_steps=ssf_steps[s, pi], stream=st.cuda_stream)
-        for st in streams[1:]:
-            e2 = torch.cuda.Event()
-            e2.record(st)
-            main.wait_event(e2)
+    # ---- phase 3: isolated launches (one stream) for per-kernel durations ----
+    iso = {}
+    for prec, dset in [(args.precision, decs)] + ([(variant[0], variant[4])] if variant else []):
+        for d in dset:
+            d.set_timing(args.iso_steps)
+        run.timed(dset, args.iso_steps, run.streams[:1], warm=False)  # every launch is timed
+        bp_ms = np.zeros((args.iso_steps, P))
+        ssf_ms = np.zeros((args.iso_steps, P))
+        for pi, d in enumerate(dset):
+            a, c = d.read_timing()
+            bp_ms[:, pi] = a[:args.iso_steps]
+            ssf_ms[:, pi] = c[:args.iso_steps]
+        it_iso = run.iters[args.warmup:args.warmup + args.iso_steps].to(torch.int64).sum(dim=2).cpu().numpy()
+        iso[prec] = (bp_ms, ssf_ms, it_iso)
 
-    for s in range(args.warmup):
-        step(s)
-    torch.cuda.synchronize()
-    # HIP events recorded by the library on the launch stream right before the
-    # BP kernel, after it and after the SSF kernel of every timed call
-    for d in decs:
-        d.set_timing(args.steps)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(args.warmup, nsteps):
-        step(s)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-
-    # ---- per-launch kernel times and algorithmic bytes ----
-    bp_ms = np.zeros((args.steps, len(ps)))
-    ssf_ms = np.zeros((args.steps, len(ps)))
-    for pi, d in enumerate(decs):
-        a, c = d.read_timing()
-        bp_ms[:, pi] = a
-        ssf_ms[:, pi] = c
-    launch_ms = bp_ms
-    it_sum = iters[args.warmup:].to(torch.int64).sum(dim=2).cpu().numpy()  # [steps, points]
-    b_io = m + n + 1  # syndrome in + correction out + failure flag
-    bytes_per_launch = b_io * B + 16 * E * it_sum  # [steps, points]
-    achieved_gbs = float(bytes_per_launch.sum() / (launch_ms.sum() * 1e-3) / 1e9)
-
-    fails = fail[args.warmup:].to(torch.int64).sum(dim=(0, 2))
-    conv = (status[args.warmup:] & 1).to(torch.int64).sum(dim=(0, 2))
-    itp = iters[args.warmup:].to(torch.float64).mean(dim=(0, 2))
-    ssp = ssf_steps[args.warmup:].to(torch.float64).mean(dim=(0, 2))
-    if world > 1:
-        dist.all_reduce(fails)
-        dist.all_reduce(conv)
-    fails = fails.cpu().numpy()
-    conv = conv.cpu().numpy()
-    shots_per_point = args.steps * B * world
+    # ---- phase 4: sampling + decode in the timed region ----
+    sd = None
+    if not args.no_sample_phase:
+        sd_elapsed = run.timed(decs, args.steps, run.streams[:1], sampler=decs[0], warm=False)
+        sd = total_shots / sd_elapsed
 
     if rank == 0:
-        total_shots = shots_per_point * len(ps)
         value = total_shots / elapsed
+        cpu = None
+        if not args.no_cpu_baseline and world == 1 and not fake:
+            cpu = cpu_baseline(code, ps, args)
         ler = {}
         for pi, p in enumerate(ps):
-            lo, hi = wilson(int(fails[pi]), shots_per_point)
-            ler[f"{p:.6g}"] = {"failures": int(fails[pi]), "shots": shots_per_point,
-                               "ler": float(fails[pi] / shots_per_point), "wilson95": [lo, hi],
-                               "bp_converged_frac": float(conv[pi] / shots_per_point),
-                               "mean_bp_iters_rank0": float(itp[pi]),
-                               "mean_ssf_steps_rank0": float(ssp[pi]),
-                               "bp_kernel_ms_per_launch": float(bp_ms[:, pi].mean()),
-                               "ssf_kernel_ms_per_launch": float(ssf_ms[:, pi].mean())}
-        traffic = latest_traffic()
+            key = f"{p:.6g}"
+            w_h = wilson(int(fails[pi]), shots_per_point)
+            row = {"failures": int(fails[pi]), "shots": shots_per_point, "ler": float(fails[pi] / shots_per_point),
+                   "wilson95": list(w_h), "bp_converged_frac": float(conv[pi] / shots_per_point),
+                   "mean_bp_iters_rank0": float(itp[pi]), "mean_ssf_steps_rank0": float(ssp[pi]),
+                   "bp_kernel_ms_isolated": float(iso[args.precision][0][:, pi].mean()),
+                   "ssf_kernel_ms_isolated": float(iso[args.precision][1][:, pi].mean())}
+            cw = None
+            if cpu is not None:
+                cw = wilson(cpu["failures_per_point"][key], cpu["shots_per_point"])
+                row["cpu_f64"] = {"failures": cpu["failures_per_point"][key], "shots": cpu["shots_per_point"],
+                                  "wilson95": list(cw)}
+                row["overlaps_cpu_f64"] = overlap(w_h, cw)
+            if variant:
+                vw = wilson(int(variant[2][pi]), shots_per_point)
+                vr = {"failures": int(variant[2][pi]), "wilson95": list(vw),
+                      "bp_converged_frac": float(variant[3][pi] / shots_per_point),
+                      "overlaps_headline": overlap(vw, w_h)}
+                if cw is not None:
+                    vr["overlaps_cpu_f64"] = overlap(vw, cw)
+                row[variant[0]] = vr
+            ler[key] = row
+
+        bp_ms, ssf_ms, it_iso = iso[args.precision]
+        bytes_per_launch = IO_BYTES_PER_SHOT * args.batch
+        achieved = bytes_per_launch / (bp_ms.mean() * 1e-3) / 1e9
+        kname = "qdec::bp_ms_wave_kernel<" + ("double" if args.precision == "f64" else "float")
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": kname + ", 2, 4, 7, true, true, 2> (BP min-sum, lean outputs, queues BP failures)",
+                "avg_launch_ms": float(bp_ms.mean()), "launches": int(bp_ms.size),
+                "timing": "HIP events recorded by the library on the launch stream around each kernel, "
+                          "isolated phase (one stream)",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "bytes_model": f"per shot {IO_BYTES_PER_SHOT} B compulsory HBM I/O (108 B syndrome + 225 B readout in, "
+                               "fail + status + int32 iterations out); BP messages stay on chip",
+                "ssf_kernel": "qdec::ssf_wave_kernel<2, 4, 2>", "ssf_avg_launch_ms": float(ssf_ms.mean()),
+                "isolated_step_ms": float(bp_ms.sum(axis=1).mean() + ssf_ms.sum(axis=1).mean()),
+                "message_model": {"bytes_per_launch": float(16 * int(hz.nnz) * it_iso.mean()),
+                                  "note": "SURVEY §8(d): 16 B per edge per BP iteration; on-chip LDS/register "
+                                          "traffic at n=225, not HBM"}}
+        pmc = None if fake else pmc_ceilings(kname)
+        if pmc is not None:
+            src, name, k = pmc
+            dv = k["derived"]
+            roof["traffic"] = dv.get("hbm_bytes_per_dispatch")
+            roof["ceilings"] = {"source": src, "kernel": name,
+                                **{key: dv.get(key) for key in ("valu_issue_frac", "lds_frac",
+                                                                "lds_bank_conflict_ratio", "hbm_frac", "clock_ghz",
+                                                                "duration_ms", "formulas")}}
+
         result = {
             "metric": METRIC, "value": value, "unit": "shots/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic: on-device Philox sampler of the storage experiment under depolarizing_noise(p, pm=p), "
-                    "seed 20250221, distinct shots per step",
+                    "seed 20250221, distinct shots per step" + (" [FAKE DEVICE: launcher test]" if fake else ""),
             "config": {"workload": "C2: (3,4)-HGP n=225 (biregular_hgp(12,3,4,seed=1234)), R=0 (H=Hz 108x225, E=756), "
-                                   "p-sweep geomspace(1e-3,1e-1,9), BP min-sum fp32 max_iter=50 alpha_t=1-2^-t + SSF "
-                                   "(Hx flip sets) + fused logical check",
-                       "shots_per_point_per_step_per_gpu": B, "global_batch": B * len(ps) * world,
+                                   f"p-sweep geomspace(1e-3,1e-1,9), BP min-sum {args.precision} max_iter=50 "
+                                   "alpha_t=1-2^-t + SSF (Hx flip sets) + fused logical check",
+                       "shots_per_point_per_step_per_gpu": args.batch, "global_batch": args.batch * P * world,
                        "parallelism": f"shot-sharded x{world}, no collective", "streams": args.streams},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "bp_ms_wave_kernel<float, 2, 4, 7, true, true, 2> (BP min-sum, fp32, lean outputs, queues BP failures)",
-                         "avg_launch_ms": float(launch_ms.mean()),
-                         "launches": int(launch_ms.size),
-                         "ssf_kernel": "ssf_wave_kernel<2, 4, 2>", "ssf_avg_launch_ms": float(ssf_ms.mean()),
-                         "timing": "HIP events recorded by the library on the launch stream around each kernel",
-                         "algorithmic_bytes_per_launch": float(bytes_per_launch.mean()),
-                         "bytes_model": "per shot: (m+n+1)=334 B I/O + 16*E=12096 B per BP iteration"},
-            "ler": ler,
         }
-        if not args.no_cpu_baseline and world == 1:
-            result["cpu_baseline"] = cpu_baseline(code, ps, args, ler)
+        if variant:
+            vb, vs, _ = iso[variant[0]]
+            result["variants"] = [{"dtype": variant[0], "value": total_shots / variant[1],
+                                   "ms_per_step": variant[1] / args.steps * 1e3,
+                                   "bp_kernel_ms_isolated_avg": float(vb.mean()),
+                                   "ssf_kernel_ms_isolated_avg": float(vs.mean()),
+                                   "note": "same shots, same protocol; LER per point under ler[p][dtype]"}]
+        if sd is not None:
+            result["sample_and_decode"] = {"value": sd, "unit": "shots/s", "dtype": args.precision, "streams": 1,
+                                           "note": "on-device sampling inside the timed region, one stream"}
+        result["roofline"] = roof
+        if cpu is not None:
+            result["cpu_baseline"] = cpu
+        result["ler"] = ler
+        if cpu is not None:
+            result["ler_overlap_all"] = {
+                "headline_vs_cpu_f64": all(r["overlaps_cpu_f64"] for r in ler.values()),
+                "variant_vs_cpu_f64": all(r[variant[0]]["overlaps_cpu_f64"] for r in ler.values()) if variant else None}
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()

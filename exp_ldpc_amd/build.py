@@ -47,20 +47,38 @@ def _stale() -> bool:
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
     """Build the library; stamps=True builds the development variant with phase
-    timers (libqdec_hip_stamps.so, loaded with QDEC_LIB=...)."""
+    timers (libqdec_hip_stamps.so, loaded with QDEC_LIB=...).  Every source is
+    compiled to its own object in parallel (objects under build/, git-ignored),
+    then linked."""
+    from concurrent.futures import ThreadPoolExecutor
     lib = LIB.replace(".so", "_stamps.so") if stamps else LIB
     if not force and not stamps and not _stale():
         return LIB
-    tmp = lib + ".tmp"
     extra = ["-DQDEC_STAMPS"] if stamps else []
-    cmd = [_hipcc(), *FLAGS, *extra, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+    objdir = os.path.join(os.path.dirname(HERE), "build", "obj_stamps" if stamps else "obj")
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, src + ".o")
+        cmd = [_hipcc(), *cflags, *extra, "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src} ({res.returncode}):\n{res.stderr[-6000:]}")
+        if verbose and res.stderr:
+            print(res.stderr[-4000:], file=sys.stderr)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = lib + ".tmp"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", tmp, *objs]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-6000:]}")
-    if verbose and res.stderr:
-        print(res.stderr[-4000:], file=sys.stderr)
+        raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-6000:]}")
     os.replace(tmp, lib)
     return lib
 

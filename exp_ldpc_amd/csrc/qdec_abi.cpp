@@ -94,6 +94,13 @@ struct qd_graph {
     int t_cap = 0, t_count = 0;
     // min-sum wave kernel: variable (column) held by each lane slot, -1 for pads
     std::vector<int> ms_var_of_slot;
+    // workspace chain: every device-buffer decode records ws_ev on its stream after
+    // its launches; a decode on another stream waits for it first, so the queue and
+    // message scratch of one handle are never used by two streams at once, and a
+    // grow path frees a buffer only after ws_ev (the last use) has completed
+    hipEvent_t ws_ev = nullptr;
+    bool ws_ev_live = false;
+    hipStream_t ws_last = nullptr;
 };
 
 namespace {
@@ -104,6 +111,20 @@ template <typename T>
 int dcs() { return lds_stride<T, kDC>(); }
 
 void set_device(qd_graph* g) { hip_check(hipSetDevice(g->device), "hipSetDevice"); }
+
+// Workspace chain (see qd_graph::ws_ev).
+void ws_acquire(qd_graph* G, hipStream_t s) {
+    if (G->ws_ev_live && G->ws_last != s) hip_check(hipStreamWaitEvent(s, G->ws_ev, 0), "hipStreamWaitEvent");
+}
+void ws_release(qd_graph* G, hipStream_t s) {
+    if (!G->ws_ev) hip_check(hipEventCreateWithFlags(&G->ws_ev, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(G->ws_ev, s), "hipEventRecord");
+    G->ws_ev_live = true;
+    G->ws_last = s;
+}
+void ws_drain(qd_graph* G) {
+    if (G->ws_ev_live) hip_check(hipEventSynchronize(G->ws_ev), "hipEventSynchronize");
+}
 
 // Layout of the compressed-state min-sum kernel (qdec_bp_ms.h).  Variable
 // lane j = rv*64 + l scatters its k-th v2c message to element i*DRS + pos of
@@ -356,6 +377,7 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
     if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision, a.B, G->num_cus))) return;
     const DevGraph& g = G->dg;
     if (a.B > G->q_cap) {
+        ws_drain(G);  // launches still in flight may use the old queue
         if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
         G->qws = nullptr;
         G->q_cap = 0;
@@ -380,6 +402,7 @@ void* message_scratch(qd_graph* G, int method, int precision, int64_t B, size_t*
     *bytes = need;
     if (need == 0) return nullptr;
     if (need > G->mws_bytes) {
+        ws_drain(G);  // launches still in flight may use the old scratch
         if (G->mws) hip_check(hipFree(G->mws), "hipFree scratch");
         G->mws = nullptr;
         G->mws_bytes = 0;
@@ -504,6 +527,8 @@ int qd_graph_destroy(qd_graph* g) {
         if (!g) return;
         (void)hipSetDevice(g->device);
         if (g->stream) (void)hipStreamSynchronize(g->stream);
+        if (g->ws_ev_live) (void)hipEventSynchronize(g->ws_ev);
+        if (g->ws_ev) (void)hipEventDestroy(g->ws_ev);
         g->arena.release();
         g->flip_arena.release();
         g->lz_arena.release();
@@ -673,8 +698,11 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         attach_timing(G, a);
         size_t sb = 0;
         void* scr = message_scratch(G, p->method, p->precision, B, &sb);
-        const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, (hipStream_t)stream, scr, sb);
+        const hipStream_t s = (hipStream_t)stream;
+        ws_acquire(G, s);
+        const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
+        ws_release(G, s);
     });
 }
 
@@ -727,8 +755,10 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         attach_timing(G, a);
         size_t sb = 0;
         void* scr = message_scratch(G, p->method, p->precision, B, &sb);
+        ws_acquire(G, s);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
+        ws_release(G, s);
         auto d2h = [&](void* h, const Reg& r, const char* what) {
             if (h) hip_check(hipMemcpyAsync(h, dptr(r), r.bytes, hipMemcpyDeviceToHost, s), what);
         };

@@ -177,11 +177,34 @@ class Decoder:
         device pointers) on `stream` (default: torch's current stream)."""
         if stream is None:
             stream = _current_stream(self.device)
+        B = int(B)
+        llr_t = "float32" if self.precision == _abi.QD_F32 else "float64"
+        for name, t, dt, cols in (("syn", syn, "uint8", self.m), ("base", base, "uint8", self.n_data),
+                                  ("readout", readout, "uint8", self.n_data), ("x", x, "uint8", self.n),
+                                  ("corr", corr, "uint8", self.n_data), ("llr", llr, llr_t, self.n),
+                                  ("iters", iters, "int32", 1), ("status", status, "uint8", 1),
+                                  ("ssf_steps", ssf_steps, "int32", 1), ("fail", fail, "uint8", 1)):
+            self._check_device_buffer(name, t, dt, B * cols)
         prm = self._params(syn_flags, ssf)
         _abi.check(self._lib.qd_decode_batch_device(
             self._handle, C.byref(prm), int(B), _abi.ptr(syn), _abi.ptr(base), _abi.ptr(readout), _abi.ptr(x),
             _abi.ptr(corr), _abi.ptr(llr), _abi.ptr(iters), _abi.ptr(status), _abi.ptr(ssf_steps), _abi.ptr(fail),
             C.c_void_p(stream)), "qd_decode_batch_device")
+
+    def _check_device_buffer(self, name, t, dtype: str, numel: int) -> None:
+        """A torch tensor handed to a *_device call must be a contiguous tensor on
+        this decoder's GPU with the ABI's element type and at least `numel`
+        elements (raw integer pointers are passed through unchecked)."""
+        if t is None or isinstance(t, int) or not hasattr(t, "data_ptr"):
+            return
+        if not t.is_cuda or t.device.index != self.device:
+            raise ValueError(f"{name}: expected a tensor on cuda:{self.device}, got {t.device}")
+        if str(t.dtype).rsplit(".", 1)[-1] != dtype:
+            raise ValueError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: tensor must be contiguous")
+        if t.numel() < numel:
+            raise ValueError(f"{name}: {t.numel()} elements, the batch needs {numel}")
 
     def sample_storage_device(self, rounds: int, p_data: float, p_meas: float, seed: int, stream_id: int,
                               shot0: int, B: int, syn, readout, stream=None) -> None:

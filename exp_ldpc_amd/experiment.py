@@ -71,7 +71,7 @@ class BatchPipeline:
     device tensors (spacetime syndrome uint8[B,(R+1)m], readout uint8[B,n])."""
 
     def __init__(self, code, rounds: int, mode: str, bp_osd_options: Dict, priors: Tuple[float, float], *,
-                 device: int = 0, precision: str = "f32", use_x_logicals: bool = False, osd_threads: int = 0,
+                 device: int = 0, precision: str = "f64", use_x_logicals: bool = False, osd_threads: int = 0,
                  noise=None):
         if mode not in DECODER_MODES:
             raise RuntimeError("Unknown decoder operation mode")
@@ -342,7 +342,7 @@ def _steps(checks):
 
 def run_simulation(samples, code, meas_prior, data_prior, noise_model, noise_model_args, bp_osd_options, rounds,
                    decoder_mode, *, seed: int = DEFAULT_SEED, stream_id: int = 0, shot0: int = 0, device: int = 0,
-                   batch: int = 1 << 18, precision: str = "f32", stats: dict | None = None):
+                   batch: int = 1 << 18, precision: str = "f64", stats: dict | None = None):
     """Sample and decode `samples` shots on one GPU; returns a bool ndarray of
     logical-failure flags (reference run_simulation, _experiment.py:154-210,
     which returns a list of the same flags)."""
@@ -408,26 +408,48 @@ def _device_count() -> int:
 
 
 def _load_checkpoint(path):
-    """Rows of a previous run's checkpoint CSV, keyed by p (empty when absent)."""
+    """Rows of a previous run's checkpoint CSV, keyed by (p, config fingerprint)
+    (empty when absent)."""
     import pandas as pd
     if not path or not os.path.exists(path) or os.path.getsize(path) == 0:
         return {}
     df = pd.read_csv(path, float_precision="round_trip")
-    return {float(r["p_ph"]): r.to_dict() for _, r in df.iterrows()}
+    if "config_fp" not in df.columns:  # rows without a fingerprint are never reused
+        return {}
+    return {(float(r["p_ph"]), str(r["config_fp"])): r.to_dict() for _, r in df.iterrows()}
+
+
+def _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, samples, point_index) -> str:
+    """Everything a point's failure count depends on besides p: the check
+    matrices and logicals, the decoder configuration, and the sampler stream
+    (seed, point index = Philox stream id, sample count)."""
+    import hashlib
+    h = hashlib.sha1()
+    for M in (code.checks.x, code.checks.z, code.logicals.x, code.logicals.z):
+        A = sp.csr_matrix(M)
+        A.sort_indices()
+        h.update(repr(A.shape).encode())
+        h.update(np.ascontiguousarray(A.indptr, dtype=np.int64).tobytes())
+        h.update(np.ascontiguousarray(A.indices, dtype=np.int64).tobytes())
+    h.update(repr((int(rounds), str(mode), sorted((k, str(v)) for k, v in bp_osd_options.items()), str(precision),
+                   int(seed), int(samples), int(point_index))).encode())
+    return h.hexdigest()[:16]
 
 
 def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_prior, *, gpus: int | None = None,
-            seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f32", checkpoint: str | None = None,
+            seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f64", checkpoint: str | None = None,
             **kwargs):
     """Sweep the physical error rate (reference p_sweep, misc/p_sweep.py:17-40).
     Shots are sharded over `gpus` devices by index (device d decodes a
-    contiguous shot range); exactly `samples` shots per point.
+    contiguous shot range); exactly `samples` shots per point.  BP runs in
+    `precision` (default f64, ldpc v1's message precision); every row records it.
 
     checkpoint: CSV path; each finished point is appended to it at once, and a
-    restarted sweep reuses the rows already there for the same p, seed and
-    sample count (shots are a pure function of (seed, point index, shot index),
-    so a recomputed point would be identical).  The reference writes its CSV
-    only at the end (misc/p_sweep.py:78)."""
+    restarted sweep reuses a row only when its p and its configuration
+    fingerprint match (code, logicals, rounds, mode, BP/OSD options, precision,
+    seed, sample count and the point index, which is the point's Philox stream
+    id), since a recomputed point would then be identical.  The reference
+    writes its CSV only at the end (misc/p_sweep.py:78)."""
     import pandas as pd
     torch = _torch()
     done = _load_checkpoint(checkpoint)
@@ -439,8 +461,9 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
     x_steps, z_steps = _steps(code.checks)
     data = []
     for pi, p_ph in enumerate(p_values):
-        prev = done.get(float(p_ph))
-        if prev is not None and int(prev.get("samples", -1)) == samples and int(prev.get("seed", -1)) == seed:
+        fp = _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, samples, pi)
+        prev = done.get((float(p_ph), fp))
+        if prev is not None:
             data.append(prev)
             continue
         t0 = time.perf_counter()
@@ -485,6 +508,9 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
         del point["code"]
         del point["bp_osd_options"]
         point["seed"] = seed
+        point["precision"] = precision
+        point["point_index"] = pi
+        point["config_fp"] = fp
         data.append(point)
         if checkpoint:
             row = pd.DataFrame.from_records([point])
@@ -529,7 +555,8 @@ def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
     parser.add_argument("--gpus", type=int, default=None, help="GPUs to shard shots over (default: all visible)")
     parser.add_argument("--seed", type=int, default=DEFAULT_SEED, help="sampler seed (counter-based Philox)")
     parser.add_argument("--batch", type=int, default=1 << 18, help="shots per device launch")
-    parser.add_argument("--precision", choices=["f32", "f64"], default="f32", help="BP message precision")
+    parser.add_argument("--precision", choices=["f32", "f64"], default="f64",
+                        help="BP message precision (default f64, as ldpc v1; f32 is the faster stated-tolerance variant)")
     parser.add_argument("--checkpoint", type=str, default=None,
                         help="CSV that each finished point is appended to; finished points are skipped on restart")
     args = parser.parse_args(sys.argv[1:])

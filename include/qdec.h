@@ -19,7 +19,12 @@
  * 0 = OK, negative = error (message via qd_last_error(), thread-local).  The
  * library owns device copies of the graph; the caller owns every buffer it
  * passes.  A handle is used from one host thread at a time; one handle per
- * device for multi-GPU.
+ * device for multi-GPU.  Device-buffer decodes on one handle may be enqueued on
+ * different streams: the handle's SSF queue and message scratch are shared, so
+ * the library chains such calls with an event (a call waits for the previous
+ * call's kernels) and frees a grown buffer only after its last use completed.
+ * Calls on one handle therefore never run concurrently; use one handle per
+ * stream for concurrent decodes.
  */
 #ifndef QDEC_H
 #define QDEC_H

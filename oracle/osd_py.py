@@ -37,6 +37,29 @@ def _solve_pivots(Hs, s):
     return piv, A[:r, n]
 
 
+def _reduce(Hs):
+    """Greedy pivot columns of Hs and a row transform T with (T Hs)[:r, piv] = I,
+    so the solution over piv of Hs[:, piv] x = s is (T s)[:r] for every s."""
+    m, n = Hs.shape
+    A = np.concatenate([Hs % 2, np.eye(m, dtype=np.uint8)], axis=1).astype(np.uint8)
+    piv = []
+    r = 0
+    for c in range(n):
+        if r >= m:
+            break
+        rows = np.nonzero(A[r:, c])[0]
+        if rows.size == 0:
+            continue
+        p = r + rows[0]
+        A[[r, p]] = A[[p, r]]
+        mask = A[:, c].astype(bool)
+        mask[r] = False
+        A[mask] ^= A[r]
+        piv.append(c)
+        r += 1
+    return piv, A[:, n:]
+
+
 def osd_decode(H, syndrome, llr, method="osd_cs", order=0):
     """Returns (osd0, osdw) uint8[n]."""
     H = sp.csr_matrix(H).toarray() % 2
@@ -68,11 +91,19 @@ def osd_decode(H, syndrome, llr, method="osd_cs", order=0):
             cands.append([nonpiv[t] for t in range(lam) if (mask >> t) & 1])
     else:
         cands = [[c] for c in nonpiv] + [[nonpiv[a], nonpiv[b]] for a, b in itertools.combinations(range(lam), 2)]
-    for g in cands:
-        s2 = (s + Hs[:, g].sum(axis=1)) % 2
-        _, xp = _solve_pivots(Hs[:, piv], s2)  # same pivot set: full column rank
-        cand = assemble(xp, g)
-        w = int(cand.sum())
+    if not cands:
+        return osd0, best
+    # every candidate's pivot solution from one row transform of Hs[:, piv]
+    # (full column rank), in candidate order; strict improvement keeps the earlier
+    piv2, T = _reduce(Hs[:, piv])
+    assert piv2 == list(range(len(piv)))
+    r = len(piv)
+    S2 = np.repeat(s[:, None], len(cands), axis=1).astype(np.int64)
+    for ci, g in enumerate(cands):
+        S2[:, ci] += Hs[:, g].astype(np.int64).sum(axis=1)
+    XP = (T.astype(np.int64) @ (S2 % 2)) % 2
+    for ci, g in enumerate(cands):
+        w = int(XP[:r, ci].sum()) + len(g)
         if w < best_w:
-            best, best_w = cand, w
+            best, best_w = assemble(XP[:r, ci].astype(np.uint8), g), w
     return osd0, best

@@ -92,8 +92,9 @@ def test_decoder_modes_run_and_agree_with_per_shot_api(gpu_available, mode, roun
     lz = code.logicals.z
     assert np.array_equal(res.fail, (((rd_h ^ corr).astype(int) @ lz.T.astype(int)) % 2).any(1))
     if mode.startswith("bposd"):
-        # OSD always returns a correction satisfying the final-round syndrome
-        assert not (((HZ @ (rd_h ^ corr).T).T % 2).any(1) & ~res.fail).any() or True
+        # BP+OSD always returns a correction that satisfies the final-round
+        # syndrome: H_st x = sigma sums over the row blocks to Hz fold(x) = Hz readout
+        assert not ((HZ @ (rd_h ^ corr).T).T % 2).any()
     # the reference-style per-shot wrapper gives the same correction for shot 0
     cls = {"bposd": BPOSDCorrect, "bposd_hybrid": BPOSDHybridCorrect, "bposd_single_shot": BPOSDCorrectSingleShot,
            "bpssf": BPSSFCorrect, "bpssf_hybrid": BPSSFHybridCorrect}.get(mode)
@@ -114,16 +115,17 @@ def test_bpssf_matches_oracle_end_to_end(gpu_available, oracle_lib):
     prior = lambda p, _, __: 2 * p / 3
     p = 0.015
     fails = run_simulation(5000, code, lambda a, b: prior(p, a, b), lambda a, b: prior(p, a, b), depolarizing_noise,
-                           {"p": p, "pm": p}, opts, 0, "bpssf", seed=3, batch=2048)
+                           {"p": p, "pm": p}, opts, 0, "bpssf", seed=3, batch=2048, precision="f32")
     syn, rd = oracle_lib.sample_storage(code.checks.z, 0, p, p, seed=3, stream=0, shot0=0, B=5000)
     ref = oracle_lib.decode(code.checks.z, 2 * p / 3, syn, method="ms", precision="f32", max_iter=50, ssf=True,
                             gens=code.checks.x, lz=code.logicals.z, readout=rd, want_llr=False, ssf_impl="fast")
     assert np.array_equal(fails, ref["fail"].astype(bool))
 
 
+@pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("p", [0.005, 0.02])
-def test_ler_overlaps_cpu_oracle_fp64(gpu_available, oracle_lib, p):
-    """GPU fp32 BP+SSF vs CPU fp64 (ldpc-like) BP+SSF on independent shots:
+def test_ler_overlaps_cpu_oracle_fp64(gpu_available, oracle_lib, p, precision):
+    """GPU f32 / f64 BP+SSF vs CPU fp64 (ldpc-like) BP+SSF on independent shots:
     Wilson 95% intervals of the logical error rate overlap."""
     from exp_ldpc_amd.experiment import run_simulation
     from exp_ldpc_amd.noise_model import depolarizing_noise
@@ -132,7 +134,7 @@ def test_ler_overlaps_cpu_oracle_fp64(gpu_available, oracle_lib, p):
     N = 40000
     pr = 2 * p / 3
     g = run_simulation(N, code, lambda a, b: pr, lambda a, b: pr, depolarizing_noise, {"p": p, "pm": p}, opts, 0,
-                       "bpssf", seed=101)
+                       "bpssf", seed=101, precision=precision)
     syn, rd = oracle_lib.sample_storage(code.checks.z, 0, p, p, seed=202, stream=0, shot0=0, B=N)
     ref = oracle_lib.decode(code.checks.z, pr, syn, method="ms", precision="f64", max_iter=50, ssf=True,
                             gens=code.checks.x, lz=code.logicals.z, readout=rd, want_llr=False, ssf_impl="fast")
@@ -190,6 +192,7 @@ def test_p_sweep_cli_runs_like_reference_script(gpu_available, tmp_path):
                 "ms_scaling_factor", "osd_method", "osd_order"):
         assert col in df.columns
     assert (df["failures"] >= 0).all() and df["failures"].iloc[0] <= df["failures"].iloc[1]
+    assert list(df["precision"]) == ["f64", "f64"]  # ldpc v1's precision by default, labelled per row
 
 
 @pytest.mark.parametrize("rounds", [0, 1])
@@ -206,7 +209,7 @@ def test_bpd_detector_mode_matches_oracle(gpu_available, oracle_lib, rounds):
     p = 0.015
     opts = {"max_iter": 40, "bp_method": "ms", "ms_scaling_factor": 0, "osd_method": "osd_cs", "osd_order": 7}
     noise = depolarizing_noise(p, p)
-    pipe = BatchPipeline(code, rounds, "bpd_detector", opts, (2 * p / 3, 2 * p / 3), noise=noise)
+    pipe = BatchPipeline(code, rounds, "bpd_detector", opts, (2 * p / 3, 2 * p / 3), noise=noise, precision="f32")
     sim = build_storage_simulation(rounds, noise, code)
     syn, rd = sim.sample_device(pipe.sampler_graph, 3000, seed=11, stream_id=0)
     res = pipe.run(syn, rd)
@@ -245,3 +248,59 @@ def test_p_sweep_checkpoint_resume(gpu_available, tmp_path):
     assert np.allclose(second["walltime"][:2], first["walltime"], rtol=1e-9, atol=0)  # reused, not recomputed
     fresh = p_sweep(p_values=[0.01, 0.02, 0.03], **{**kw, "checkpoint": None})  # same point indices (streams)
     assert list(second["failures"]) == list(fresh["failures"])
+
+
+def _raw_history(syn, R, m):
+    """Undo the spacetime differencing (spacetime_code.py:98-119): s_t = xor of sigma_0..sigma_t."""
+    sv = syn.reshape(syn.shape[0], R + 1, m)
+    return np.bitwise_xor.accumulate(sv, axis=1)[:, :R]
+
+
+@pytest.mark.parametrize("bp_method", ["ms", "ps"])
+def test_single_shot_matches_oracle_loop(gpu_available, oracle_lib, bp_method):
+    """bposd_single_shot at R=2: corrections and failure flags == the CPU
+    restatement of BPOSDCorrectSingleShot.readout_correction
+    (/root/reference/python/qldpc/misc/_experiment.py:43-60; oracle/harness_py.py)."""
+    from exp_ldpc_amd.experiment import BatchPipeline
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    from exp_ldpc_amd.storage_sim import build_storage_simulation
+    from oracle.harness_py import logical_failures, single_shot_corrections
+    code = load_code("hgp_12_3_4_s1234")
+    R, p = 2, 0.02
+    opts = {"max_iter": 30, "bp_method": bp_method, "ms_scaling_factor": 0, "osd_method": "osd_cs", "osd_order": 5}
+    priors = (2 * p / 3, 2 * p / 3)
+    pipe = BatchPipeline(code, R, "bposd_single_shot", opts, priors, precision="f32")
+    sim = build_storage_simulation(R, depolarizing_noise(p, p), code)
+    syn, rd = sim.sample_device(pipe.sampler_graph, 400, seed=11, stream_id=3)
+    res = pipe.run(syn, rd, want_corrections=True)
+    syn_h, rd_h = syn.cpu().numpy(), rd.cpu().numpy()
+    hist = _raw_history(syn_h, R, HZ.shape[0])
+    ref = single_shot_corrections(oracle_lib, code.checks.z, R, hist, rd_h, opts, priors, precision="f32")
+    assert np.array_equal(res.corrections, ref)
+    assert np.array_equal(res.fail, logical_failures(code.logicals.z, rd_h, ref))
+    assert res.fail.any() and not res.fail.all()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_bposd_reference_default_matches_oracle(gpu_available, oracle_lib, precision):
+    """The reference default (p_sweep: bposd, R=1, bp_method ps, max_iter 225,
+    osd_cs order 7; BASELINE config 1 at p=0.01): corrections and failure flags
+    == oracle BP (ldpc v1 product-sum restatement) + numpy OSD on H_st
+    (/root/reference/python/qldpc/misc/_experiment.py:62-83; oracle/harness_py.py)."""
+    from exp_ldpc_amd.experiment import BatchPipeline
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    from exp_ldpc_amd.storage_sim import build_storage_simulation
+    from oracle.harness_py import logical_failures, spacetime_bposd_corrections
+    code = load_code("hgp_12_3_4_s1234")
+    R, p = 1, 0.01
+    opts = {"max_iter": 225, "bp_method": "ps", "ms_scaling_factor": 0, "osd_method": "osd_cs", "osd_order": 7}
+    priors = (2 * p / 3, 2 * p / 3)
+    pipe = BatchPipeline(code, R, "bposd", opts, priors, precision=precision)
+    sim = build_storage_simulation(R, depolarizing_noise(p, p), code)
+    syn, rd = sim.sample_device(pipe.sampler_graph, 3000, seed=1, stream_id=7)
+    res = pipe.run(syn, rd, want_corrections=True)
+    syn_h, rd_h = syn.cpu().numpy(), rd.cpu().numpy()
+    ref = spacetime_bposd_corrections(oracle_lib, code.checks.z, R, syn_h, opts, priors, precision=precision)
+    assert np.array_equal(res.corrections, ref)
+    assert np.array_equal(res.fail, logical_failures(code.logicals.z, rd_h, ref))
+    assert res.bp_converged < 3000  # OSD ran
