@@ -35,6 +35,7 @@
 // (popcount of xor with a per-subset mask: 5 VALU ops per subset).  A wave max
 // picks the flip.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "qdec_device.h"
 #include "qdec_bp_ms.h"
@@ -602,11 +603,20 @@ static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, 
 
 template <typename K>
 static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
-                             const DecodeArgs& a, int block = 64) {
+                             const DecodeArgs& a, int block = 64, int max_per_cu = 0) {
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    static const int cap = [] {  // diagnostics: QDEC_MAX_BLOCKS_PER_CU caps the persistent grid
+        const char* v = std::getenv("QDEC_MAX_BLOCKS_PER_CU");
+        return v ? std::atoi(v) : 0;
+    }();
+    if (cap > 0 && per_cu > cap) per_cu = cap;
+    if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
+    // one-wave blocks: a multiple of 4 per CU puts the same number of waves on
+    // every SIMD (11 f64 waves would sit 3/3/3/2 and run slower than 8)
+    if (block == 64 && per_cu > 4) per_cu &= ~3;
     long long grid = (long long)num_cus * per_cu;
     if (grid > work) grid = work;
     if (grid <= 0) return 0;
@@ -620,21 +630,30 @@ template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
 static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if constexpr (METHOD == 1) {
         const size_t lds = MsLds<T>::template bytes<RC, RV>(g);
+        if (a.wave_ctr) {  // ShotSeq's chunk counter
+            const hipError_t e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);
+            if (e != hipSuccess) return (int)e;
+        }
         const bool lean = !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1 &&
                           (!DEFER || a.q_packed);
+        // f64: 2 waves per SIMD measured faster than 3 at every p (n = 225: 8.5 vs
+        // 10.3 ms per 2^18 shots at p = 0.1, 0.51 vs 0.66 at p = 0.001)
+        constexpr int cap = sizeof(T) == 8 ? 8 : 0;
         // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
             if (g.ms_d3r >= 2) {
                 if (lean)
                     return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 2>, lds, a.B, num_cus,
-                                             stream, g, a);
+                                             stream, g, a, 64, cap);
                 return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 2>, lds, a.B, num_cus,
-                                         stream, g, a);
+                                         stream, g, a, 64, cap);
             }
         }
         if (lean)
-            return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 0>, lds, a.B, num_cus, stream, g, a);
-        return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 0>, lds, a.B, num_cus, stream, g, a);
+            return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 0>, lds, a.B, num_cus, stream, g, a,
+                                     64, cap);
+        return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 0>, lds, a.B, num_cus, stream, g, a,
+                                 64, cap);
     } else {
         const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
         return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, DEFER>, lds, a.B, num_cus, stream, g, a);

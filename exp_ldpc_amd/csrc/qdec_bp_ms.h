@@ -39,20 +39,41 @@ struct FBits<double> {
     __device__ static double from(U u) { return __longlong_as_double((long long)u); }
 };
 
+// f64 min/max on the VALU without the IEEE canonicalisation of the operands
+// (finite, non-NaN inputs only): max(a, |b|), min(a, |b|), min(a, b).
+__device__ __forceinline__ double max_abs_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double min_abs_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double min_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // LDS carve-up (elements of T, then bytes)
 template <typename T>
 struct MsLds {
     static constexpr int DRS = lds_stride<T, kDR>();
-    __host__ __device__ static size_t v2c_elems(int m_pad) { return ((size_t)m_pad * DRS + 64 + 1) / 2 * 2; }
+    // v2c rows: the m checks plus one all-Big row (index m) that every pad check
+    // lane reads; then the 64 dummy elements pad edges scatter into
+    __host__ __device__ static int rows(const DevGraph& g) { return g.m + 1; }
+    __host__ __device__ static size_t v2c_elems(int nrows) { return ((size_t)nrows * DRS + 64 + 1) / 2 * 2; }
     __host__ __device__ static size_t state_elems(int m_pad) {
         return ((size_t)2 * (m_pad + 1) * sizeof(T) + 15) / 16 * 16 / sizeof(T);
     }
-    __host__ __device__ static size_t core_bytes(int m_pad, int n_pad) {
-        return ((v2c_elems(m_pad) + state_elems(m_pad)) * sizeof(T) + (size_t)n_pad + 64 + 15) / 16 * 16;
+    __host__ __device__ static size_t core_bytes(const DevGraph& g) {
+        return ((v2c_elems(rows(g)) + state_elems(g.m_pad)) * sizeof(T) + (size_t)g.n_pad + 64 + 15) / 16 * 16;
     }
     template <int RC, int RV>
     __host__ __device__ static size_t bytes(const DevGraph& g) {
-        return core_bytes(g.m_pad, g.n_pad) + ShotIo<RC, RV>::bytes(g);
+        return core_bytes(g) + ShotIo<RC, RV>::bytes(g);
     }
 };
 
@@ -72,12 +93,56 @@ __device__ __forceinline__ T alpha_bits(int it, double ms_scaling) {
     }
 }
 
+// Shot order of a persistent wave (guided scheduling): the first ~80 % of the
+// batch by a static stride (no atomics), the rest handed out in chunks of kChunk
+// shots from a counter (a.wave_ctr, zeroed by the launcher), so waves that drew
+// cheap shots or sit on a less loaded SIMD take more of the tail.  The counter
+// result for the following chunk is requested when a chunk is started and read
+// kChunk shots later (its latency hidden by a shot's work).  Every shot < B is
+// produced exactly once; indices >= B end the wave's loop.
+struct ShotSeq {
+    static constexpr int kChunk = 4;
+    int64_t t = 0, rounds0 = 0, base = 0, grid = 1, blk = 0;
+    int left = 0;
+    unsigned long long pend = 0;  // lane 0: prefetched chunk id
+    unsigned long long* ctr = nullptr;
+    bool have = false;
+    __device__ ShotSeq(const DecodeArgs& a, int lane) {
+        grid = gridDim.x;
+        blk = blockIdx.x;
+        ctr = a.wave_ctr;
+        rounds0 = ctr ? (a.B * 4 / 5) / grid : (a.B + grid - 1) / grid + 1;
+        if (ctr && rounds0 == 0) request(lane);
+    }
+    __device__ void request(int lane) {
+        if (lane == 0) pend = atomicAdd(ctr, 1ull);
+        have = true;
+    }
+    __device__ int64_t next(int lane) {
+        if (t < rounds0) {
+            const int64_t s = blk + t * grid;
+            if (++t == rounds0 && ctr) request(lane);
+            return s;
+        }
+        if (left == 0) {
+            const unsigned long long c = __builtin_amdgcn_readfirstlane((unsigned)pend) |
+                                         ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pend >> 32)) << 32);
+            base = rounds0 * grid + (int64_t)c * kChunk;
+            left = kChunk;
+            request(lane);
+        }
+        return base + (kChunk - left--);
+    }
+};
+
 // LEAN: the throughput configuration (no x / corr / llr outputs, no base, no
 // syndrome flags, no spacetime fold): the per-shot epilogue is the ballot-word
 // failure check only, which keeps the kernel's scalar state small.
 // D3R: leading variable rounds whose slots all have degree <= 3.
+// f64: launched at 2 waves per SIMD (launch_bp_wave caps the grid; measured
+// faster than 3), so the register budget is 256; f32: 4 waves (<= 128 VGPRs).
 template <typename T, int RC, int RV, int DRC, bool DEFER, bool LEAN, int D3R>
-__global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(DevGraph g, DecodeArgs a) {
     static_assert(DRC <= kDR, "compute width exceeds the LDS row");
     static_assert(D3R <= RV, "degree rounds");
     using V2 = __attribute__((ext_vector_type(2))) T;
@@ -90,9 +155,9 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
     constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* v2c = reinterpret_cast<T*>(smem);
-    T* st = v2c + MsLds<T>::v2c_elems(g.m_pad);
+    T* st = v2c + MsLds<T>::v2c_elems(MsLds<T>::rows(g));
     uint8_t* xh = reinterpret_cast<uint8_t*>(st + MsLds<T>::state_elems(g.m_pad));
-    Io io(g, smem + MsLds<T>::core_bytes(g.m_pad, g.n_pad));
+    Io io(g, smem + MsLds<T>::core_bytes(g));
 
     const int lane = threadIdx.x;
     const int m = g.m, n = g.n;
@@ -112,6 +177,9 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
         else vsl[rv / 2] |= (uint32_t)g.ms_vslot[sl] << 16;
     }
     auto col_of = [&](int rv) -> int { return (int)((vsl[rv / 2] >> (16 * (rv % 2))) & 0xffffu); };
+    int sslot[RC];  // where this lane's checks write their state (host-placed)
+#pragma unroll
+    for (int rc = 0; rc < RC; ++rc) sslot[rc] = g.ms_sslot[PREC][rc * 64 + lane];
     uint64_t smask[RC][RV];
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc)
@@ -120,11 +188,14 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
 
     // one-time LDS init: unused row positions hold Big forever (never the
     // minimum, positive sign), state m_pad is the zero state of pad edges
-    for (int e = lane; e < (int)MsLds<T>::v2c_elems(g.m_pad); e += 64) v2c[e] = Big<T>::v;
+    for (int e = lane; e < (int)MsLds<T>::v2c_elems(MsLds<T>::rows(g)); e += 64) v2c[e] = Big<T>::v;
     for (int e = lane; e < (int)MsLds<T>::state_elems(g.m_pad); e += 64) st[e] = (T)0;
     for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
     io.init(g, lane);
-    io.stage(g, a, blockIdx.x, 0, lane);
+    ShotSeq seq(a, lane);
+    int64_t shot = seq.next(lane);
+    io.stage(g, a, shot, 0, lane);
+    int64_t nxt = seq.next(lane);
     wave_lds_sync();
 
     int buf = 0;
@@ -132,7 +203,7 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
 #ifdef QDEC_STAMPS
     const unsigned long long qdec_t0 = __builtin_amdgcn_s_memtime(), qdec_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (int64_t shot = blockIdx.x; shot < a.B; shot += gridDim.x, buf ^= 1) {
+    for (; shot < a.B; buf ^= 1) {
         // ---- syndrome (staged one shot ahead: at least the NR readout loads of
         // the same stage are younger); then stage the next shot ----
         QDEC_STAMP(5);
@@ -148,7 +219,8 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
             sbit[rc] = (i < m && a.syn) ? (srow[i] & 1) != 0 : false;
         }
         wait_lds();
-        io.stage(g, a, shot + gridDim.x, buf ^ 1, lane);
+        const int64_t nn = seq.next(lane);  // any counter request is older than the stage
+        io.stage(g, a, nxt, buf ^ 1, lane);
         if (!LEAN && a.syn_flags) {
             const bool use_b = (a.syn_flags & 1) && a.base;
             const bool use_r = (a.syn_flags & 2) && a.readout;
@@ -196,26 +268,32 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
             // ---- check pass: state (m1, m2) with the parity in both signs ----
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
-                const int i = rc * 64 + lane;
+                const int i = min(rc * 64 + lane, m);  // pad check lanes share the Big row m
                 T v[kDR];
                 lds_load<T, kDR>(v2c + i * DRS, v);
                 T m1 = Big<T>::v, m2 = Big<T>::v;
                 bool par = sbit[rc];
 #pragma unroll
                 for (int k = 0; k < DRC; ++k) {
-                    const T av = fabs(v[k]);
-                    m2 = med3(av, m1, m2);
-                    if constexpr (sizeof(T) == 4)
+                    if constexpr (sizeof(T) == 4) {
+                        const T av = fabs(v[k]);
+                        m2 = med3(av, m1, m2);
                         m1 = med3(av, m1, -Big<T>::v);  // true median = min(|v|, m1): one VALU, abs modifier
-                    else
-                        m1 = fmin(m1, av);
+                    } else {
+                        // second minimum = min(m2, max(m1, |v|)), minimum = min(m1, |v|): three f64
+                        // ops with the abs source modifier; written out because the IEEE
+                        // fmin/fmax lowering first canonicalises |v| (a fourth f64 op).
+                        // Messages are finite, so no NaN reaches these.
+                        m2 = min_f64(m2, max_abs_f64(m1, v[k]));
+                        m1 = min_abs_f64(m1, v[k]);
+                    }
                     par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign (s_xor of compare masks)
                 }
                 // both minima carry the parity in their sign bit (they are >= +0)
                 V2 s2;
                 s2.x = par ? -m1 : m1;
                 s2.y = par ? -m2 : m2;
-                *reinterpret_cast<V2*>(st + 2 * i) = s2;
+                *reinterpret_cast<V2*>(st + 2 * sslot[rc]) = s2;
             }
             wave_lds_sync();
 
@@ -371,6 +449,8 @@ __global__ __launch_bounds__(64, 4) void bp_ms_wave_kernel(DevGraph g, DecodeArg
         }
         wave_lds_sync();
         QDEC_STAMP(4);
+        shot = nxt;
+        nxt = nn;
     }
 #ifdef QDEC_STAMPS
     QDEC_COUNT(10, __builtin_amdgcn_s_memtime() - qdec_t0);

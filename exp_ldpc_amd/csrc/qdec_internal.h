@@ -66,9 +66,11 @@ struct DevGraph {
     // sit in lane slots sorted by degree (ms_vslot); slot edge k scatters its v2c
     // message to element (etab & 0xffff) and gathers check state (etab >> 16);
     // pads -> a dummy element / the zero state m_pad.
-    // Row positions inside a check's v2c row are chosen on the host so the
-    // scatter has at most 2-way bank conflicts (ms_layout in qdec_abi.cpp).
+    // Row positions inside a check's v2c row and the state slot of each check
+    // are chosen on the host (per precision) to cut the LDS bank conflicts of
+    // the scatter and of the state gather (ms_layout in qdec_abi.cpp).
     const uint32_t* ms_etab[2];   // [kDC][n_pad], per precision (element strides differ)
+    const uint16_t* ms_sslot[2];  // [m_pad] state slot written by check lane i, per precision
     const uint64_t* ms_smask;     // [n_pad/64][m_pad] slots of check i's columns inside 64-slot word w
     const uint16_t* ms_vslot;     // [n_pad] column held by lane slot s (pads: n_pad + s % 64)
     const void* ms_prior[2];      // [precision][n_pad] min-sum priors in slot order
@@ -121,6 +123,9 @@ struct DecodeArgs {
     // shots dynamically (a straggler does not hold up a fixed stride of shots);
     // nullptr -> static stride.  Set by the launcher.
     unsigned long long* work_ctr;
+    // min-sum wave kernel: counter of the dynamically scheduled shot chunks
+    // (ShotSeq, qdec_bp_ms.h); zeroed by the launcher; nullptr -> static stride
+    unsigned long long* wave_ctr;
     // optional timing (host side only): events recorded on the launch stream
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr
