@@ -45,17 +45,19 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, stamps: bool = False, defines=(), tag: str = "") -> str:
     """Build the library; stamps=True builds the development variant with phase
-    timers (libqdec_hip_stamps.so, loaded with QDEC_LIB=...).  Every source is
-    compiled to its own object in parallel (objects under build/, git-ignored),
+    timers (libqdec_hip_stamps.so), `defines` + `tag` a development variant
+    (libqdec_hip_<tag>.so); variants are loaded with QDEC_LIB=....  Every source
+    is compiled to its own object in parallel (objects under build/, git-ignored),
     then linked."""
     from concurrent.futures import ThreadPoolExecutor
-    lib = LIB.replace(".so", "_stamps.so") if stamps else LIB
-    if not force and not stamps and not _stale():
+    suffix = ("_stamps" if stamps else "") + (f"_{tag}" if tag else "")
+    lib = LIB.replace(".so", suffix + ".so")
+    if not force and not suffix and not _stale():
         return LIB
-    extra = ["-DQDEC_STAMPS"] if stamps else []
-    objdir = os.path.join(os.path.dirname(HERE), "build", "obj_stamps" if stamps else "obj")
+    extra = (["-DQDEC_STAMPS"] if stamps else []) + [f"-D{d}" for d in defines]
+    objdir = os.path.join(os.path.dirname(HERE), "build", "obj" + suffix)
     os.makedirs(objdir, exist_ok=True)
     cflags = [f for f in FLAGS if f != "-shared"]
 
@@ -84,4 +86,8 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))
+    # python -m exp_ldpc_amd.build [--force] [--stamps] [--tag T -DNAME=V ...]
+    argv = sys.argv[1:]
+    tag = argv[argv.index("--tag") + 1] if "--tag" in argv else ""
+    defs = [a[2:] for a in argv if a.startswith("-D")]
+    print(build(force="--force" in argv, verbose=True, stamps="--stamps" in argv, defines=defs, tag=tag))

@@ -305,6 +305,9 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 //   4. the flip updates the residual (u32 per check in LDS) and hard decision.
 // Key (int32): score << 15 | (127 - g) << 8; |score| <= 32*840 < 2^15, g < 128.
 constexpr int kSsfWaves = 4;
+#ifndef QDEC_SSF_OCC
+#define QDEC_SSF_OCC 4  // minimum waves per SIMD the SSF kernel is compiled for
+#endif
 
 template <int RG>
 struct SsfLds {
@@ -329,7 +332,7 @@ struct SsfLds {
 // XW/RW: words of the packed queue entries (hard decision by column, residual
 // by check) written by the wave BP kernels (queue_push_packed).
 template <int RG, int XW, int RW>
-__global__ __launch_bounds__(64 * kSsfWaves, 4) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
     constexpr int GP = SsfLds<RG>::GP;
     constexpr int QW = QEntry<XW, RW>::QW;
     static_assert(2 * QW <= 64, "entry staging");

@@ -746,8 +746,10 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
         const size_t per_wg = block_slice_bytes(g, sizeof(T), placement);
         if (!scratch || per_wg == 0 || scratch_bytes <= kLaneHeader) return (int)hipErrorInvalidValue;
         const long long max_wg = (long long)((scratch_bytes - kLaneHeader) / per_wg);
-        if (max_wg < 1) return (int)hipErrorOutOfMemory;
-        cap = (int)std::max<long long>(1, max_wg / num_cus);
+        // the grid is num_cus * cap workgroups, each owning one slice: at least
+        // one slice per CU (block_scratch_bytes sizes 4 per CU)
+        if (max_wg < num_cus) return (int)hipErrorOutOfMemory;
+        cap = (int)(max_wg / num_cus);
         a.work_ctr = static_cast<unsigned long long*>(scratch);
         gs = reinterpret_cast<T*>(static_cast<unsigned char*>(scratch) + kLaneHeader);
         const hipError_t e0 = hipMemsetAsync(a.work_ctr, 0, sizeof(unsigned long long), stream);

@@ -146,3 +146,16 @@ def test_psl13_lift_spacetime_r1_parity(gpu_available, oracle_lib, psl13_hz, ker
     syn, rd = oracle_lib.sample_storage(hz, 1, p, p, seed=SEED, stream=8, shot0=0, B=24)
     _decode_both(oracle_lib, H, 2 * p / 3, syn, max_iter=10, keys=("corr", "iters", "status"),
                  n_data=hz.shape[1], fold_blocks=2)
+
+
+def test_psl13_spacetime_r1_product_sum_f32(gpu_available, oracle_lib, psl13_hz):
+    """Product-sum f32 on the placement-0 graph (shot state in HBM, hard-decision
+    bits in LDS): the reference CLI default bp_method with the p_sweep-style f32
+    variant, x / iterations / status bit-exact, corrections folded at R = 1."""
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    hz = psl13_hz
+    H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
+    p = 0.005
+    syn, rd = oracle_lib.sample_storage(hz, 1, p, p, seed=SEED, stream=9, shot0=0, B=12)
+    _decode_both(oracle_lib, H, 2 * p / 3, syn, max_iter=8, method="ps", precision="f32",
+                 keys=("x", "corr", "iters", "status"), n_data=hz.shape[1], fold_blocks=2)

@@ -214,7 +214,7 @@ BLOCK_GRAPHS = ["hgp_24_3_4_s11", "hgp_36_3_4_s42_g4", "st2_hgp_12_3_4_s1234", "
 
 
 @pytest.mark.parametrize("name", BLOCK_GRAPHS)
-@pytest.mark.parametrize("method,precision", [("ms", "f32"), ("ps", "f64"), ("ms", "f64")])
+@pytest.mark.parametrize("method,precision", [("ms", "f32"), ("ps", "f32"), ("ps", "f64"), ("ms", "f64")])
 def test_block_kernel_parity(gpu_available, oracle_lib, name, method, precision):
     """Graphs outside the wave shapes (n > 576, row degree 9 at R >= 2, HBM
     message scratch for the 36x36 spacetime graph) take the workgroup kernels."""
