@@ -16,7 +16,7 @@ This module supplies the two pieces without Stim:
   does.  Decomposition separators ``^`` are dropped: the reference keeps the
   union of an error's targets (``spacetime_code.py:157-158``).
 * ``storage_experiment_dem`` writes the DEM of the storage experiment's Z
-  sector for R = 0 / 1 under ``depolarizing_noise(p, pm)`` from the circuit's
+  sector for any R under ``depolarizing_noise(p, pm)`` from the circuit's
   noise semantics: X components of data DEPOLARIZE1 (2p/3 per
   event, the rate the reference's priors use, ``scripts/p_sweep.py:4-5``) and
   measurement / readout flips (pm).  Detectors are those of
@@ -172,34 +172,52 @@ class DetectorSpacetimeCode:
 
 
 def storage_experiment_dem(hz, lz, rounds: int, p: float, pm: float | None = None) -> str:
-    """DEM text of the storage experiment's Z sector for rounds in {0, 1} (module
-    docstring).  D0..D(m-1) are the first-round Z detectors when R = 1
-    (storage_sim.py:146-147), then the final-round detectors (:176-179);
-    observable i is LZ row i (:180-182)."""
-    if rounds not in (0, 1):
-        raise NotImplementedError("storage_experiment_dem covers rounds 0 and 1")
+    """DEM text of the storage experiment's Z sector for any R >= 0 (module
+    docstring).  Detector block t (rows t*m ..) is the differenced Z syndrome of
+    round t (storage_sim.py:146-179: first-round detectors, then s_t ^ s_{t-1}),
+    block R the final readout's Hz parities against the last round; observable i
+    is LZ row i (:180-182).
+
+    Fault columns follow the circuit's noise events in time order (the
+    schedule the sampler restates: noise_model.py:163-193 on storage_sim.py:110-199,
+    including the REPEAT-body DEPOLARIZE1 of rounds t >= 1):
+      for t < R: the data error before round t's Z readout (flips block t),
+                 round t's Z measurement flips (blocks t and t+1),
+                 the data error after the readout (block t+1), and for t >= 1 the
+                 one the rewriter places at the end of the REPEAT body (block t+1);
+      then the readout flips (block R).  R = 0 has one data event and the readout.
+    A data X error in slot t flips every later syndrome and the readout, so it
+    fires only detector block t and the observables."""
+    if rounds < 0:
+        raise ValueError("rounds must be >= 0")
     pm = p if pm is None else pm
     hz = sp.csc_matrix(hz)
     lz = sp.csc_matrix(np.asarray(lz.todense() if sp.issparse(lz) else lz) % 2)
     m, n = hz.shape
     px = 2 * p / 3
-    final0 = m * rounds
+    R = rounds
     col = lambda M, j: M.indices[M.indptr[j]:M.indptr[j + 1]].tolist()
     lines = []
 
     def err(prob, dets, obs):
         lines.append(("error(%r) " % float(prob) + " ".join([f"D{d}" for d in dets] + [f"L{o}" for o in obs])).rstrip())
 
-    if rounds == 1:
-        for j in range(n):  # data X error before the round: first-round detectors; cancels in the final difference
-            err(px, col(hz, j), col(lz, j))
-        for i in range(m):  # Z-check measurement flip: first-round detector i and final detector i
-            err(pm, [i, final0 + i], [])
-    for j in range(n):      # data X error after the last measurement round (R = 0: the only one)
-        err(px, [final0 + d for d in col(hz, j)], col(lz, j))
-    for j in range(n):      # readout flip of data qubit j
-        err(pm, [final0 + d for d in col(hz, j)], col(lz, j))
-    lines += [f"detector D{i}" for i in range(m * (rounds + 1))]
+    def data_slot(t):
+        for j in range(n):
+            err(px, [t * m + d for d in col(hz, j)], col(lz, j))
+
+    for t in range(R):
+        data_slot(t)                      # before round t's Z readout
+        for i in range(m):                # Z-check measurement flip of round t
+            err(pm, [t * m + i, (t + 1) * m + i], [])
+        data_slot(t + 1)                  # after the readout
+        if t >= 1:
+            data_slot(t + 1)              # end of the REPEAT body (noise_model.py:183-189)
+    if R == 0:
+        data_slot(0)                      # single timestep: noise, then the final MZ
+    for j in range(n):                    # readout flip of data qubit j
+        err(pm, [R * m + d for d in col(hz, j)], col(lz, j))
+    lines += [f"detector D{i}" for i in range(m * (R + 1))]
     lines += [f"logical_observable L{o}" for o in range(lz.shape[0])]
     return "\n".join(lines) + "\n"
 

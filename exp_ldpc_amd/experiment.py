@@ -14,7 +14,7 @@ device.  Decoder modes (``--decoder_mode``):
   bp                 BP only on the spacetime matrix
   bpd_detector       BP on the fault check matrix of a detector error model
                      (_experiment.py:128-151); the storage experiment's DEM is
-                     written by dem.storage_experiment_dem (R = 0 / 1)
+                     written by dem.storage_experiment_dem (any R)
 
 OSD runs on the GPU for the shots BP did not converge on (Decoder.osd_device,
 csrc/qdec_osd.hip), fused with the fold and the failure check; graphs too large

@@ -195,7 +195,7 @@ def test_p_sweep_cli_runs_like_reference_script(gpu_available, tmp_path):
     assert list(df["precision"]) == ["f64", "f64"]  # ldpc v1's precision by default, labelled per row
 
 
-@pytest.mark.parametrize("rounds", [0, 1])
+@pytest.mark.parametrize("rounds", [0, 1, 2, 3])
 def test_bpd_detector_mode_matches_oracle(gpu_available, oracle_lib, rounds):
     """bpd_detector (reference BPDetectorCorrect, _experiment.py:128-151): BP on the
     storage DEM's fault check matrix with its fault priors; failure flags equal the
