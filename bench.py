@@ -13,8 +13,12 @@ message precision (its loops use double).  The same shots are then decoded in
 f32 (the stated-tolerance variant) and reported under `variants`.
 
 Phases (rank 0 prints ONE JSON line):
-  1. headline: W warmup + K timed steps, the 9 points spread over --streams HIP
-     streams (one point's SSF kernel overlaps another point's BP kernel);
+  1. headline: W warmup + K timed steps, the 9 points round-robin over --streams
+     HIP streams, so kernels of independent points fill each other's tails
+     (--schedule pipeline: every BP kernel on one stream and every SSF kernel on
+     a second one behind an event -- measured slower: the persistent BP kernel
+     fills every CU, so SSF only runs in BP's tail, which it cannot fill because
+     it depends on that same BP kernel);
   2. f32 variant: the same shots, same timing protocol;
   3. isolated launches (--iso-steps, one stream): per-kernel durations from HIP
      events the library records on the launch stream around each kernel; the
@@ -182,11 +186,14 @@ class Run:
         self.status = torch.empty((self.nsteps, P, self.B), **u8)
         self.fail = torch.empty((self.nsteps, P, self.B), **u8)
         self.ssf_steps = torch.empty((self.nsteps, P, self.B), dtype=torch.int32, device=dev)
+        self.ssf_stream = None
         if fake:
             self.streams = [None]
         else:
             main = torch.cuda.current_stream(dev)
             self.streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
+            if args.schedule == "pipeline":
+                self.ssf_stream = torch.cuda.Stream(dev)
 
     def shot0(self, s):
         return (s * self.world + self.rank) * self.B
@@ -205,8 +212,26 @@ class Run:
             import torch.distributed as dist
             dist.barrier()
 
+    def pipelined(self, decs, on: bool):
+        """Route (or stop routing) the decoders' SSF kernels to the SSF stream."""
+        if self.fake or self.ssf_stream is None:
+            return
+        for d in decs:
+            d.set_ssf_stream(self.ssf_stream if on else None)
+
     def step(self, decs, s, streams):
         torch = self.torch
+        if not self.fake and self.ssf_stream is not None and len(streams) > 1:
+            # pipeline: BP kernels in point order on the main stream, each SSF on
+            # the SSF stream behind its BP kernel; the main stream rejoins at the end
+            for pi in range(len(self.ps)):
+                decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
+                                       status=self.status[s, pi], fail=self.fail[s, pi],
+                                       ssf_steps=self.ssf_steps[s, pi], stream=streams[0].cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.ssf_stream)
+            streams[0].wait_event(ev)
+            return
         if self.fake or len(streams) == 1:
             for pi in range(len(self.ps)):
                 decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
@@ -280,7 +305,12 @@ def main():
                     help="second precision decoded on the same shots (reported under variants)")
     ap.add_argument("--cpu-shots", type=int, default=200000, help="CPU-baseline shots per sweep point")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=5, help="HIP streams the sweep points are spread over")
+    ap.add_argument("--streams", type=int, default=5, help="HIP streams the sweep points are spread over "
+                                                           "(--schedule streams)")
+    ap.add_argument("--schedule", default="streams", choices=["pipeline", "streams"],
+                    help="pipeline: every BP kernel on one stream, every SSF kernel on a second one behind an "
+                         "event (point i's SSF overlaps point i+1's BP); streams: points round-robin over "
+                         "--streams streams")
     ap.add_argument("--iso-steps", type=int, default=2, help="isolated (one-stream) steps timing each kernel")
     ap.add_argument("--no-sample-phase", action="store_true", help="skip the sampling+decode phase")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
@@ -329,8 +359,10 @@ def main():
         run.sample(decs[0], s)
     run.sync()
 
-    # ---- phase 1: headline precision, overlapped streams ----
+    # ---- phase 1: headline precision, overlapped (pipeline or streams) ----
+    run.pipelined(decs, True)
     elapsed = run.timed(decs, args.steps, run.streams)
+    run.pipelined(decs, False)
     fails, conv, itp, ssp = run.counts()
     shots_per_point = args.steps * args.batch * world
     total_shots = shots_per_point * P
@@ -339,7 +371,9 @@ def main():
     variant = None
     if args.variant not in ("none", args.precision):
         vdecs = decoders(args.variant)
+        run.pipelined(vdecs, True)
         v_elapsed = run.timed(vdecs, args.steps, run.streams)
+        run.pipelined(vdecs, False)
         v_fails, v_conv, _, _ = run.counts()
         variant = (args.variant, v_elapsed, v_fails, v_conv, vdecs)
 
@@ -432,7 +466,8 @@ def main():
                                    f"p-sweep geomspace(1e-3,1e-1,9), BP min-sum {args.precision} max_iter=50 "
                                    "alpha_t=1-2^-t + SSF (Hx flip sets) + fused logical check",
                        "shots_per_point_per_step_per_gpu": args.batch, "global_batch": args.batch * P * world,
-                       "parallelism": f"shot-sharded x{world}, no collective", "streams": args.streams},
+                       "parallelism": f"shot-sharded x{world}, no collective",
+                       "schedule": args.schedule if args.schedule == "pipeline" else f"{args.streams} streams"},
         }
         if variant:
             vb, vs, _ = iso[variant[0]]

@@ -103,6 +103,10 @@ struct qd_graph {
     bool ws_ev_live = false;
     // 256-B control block: [0] shot-chunk counter of the min-sum wave kernel
     void* ctl = nullptr;
+    // qd_graph_set_ssf_stream: SSF kernels of device-buffer decodes go to this
+    // stream behind ssf_ev (nullptr: the decode's own stream)
+    hipStream_t ssf_stream = nullptr;
+    hipEvent_t ssf_ev = nullptr;
     hipStream_t ws_last = nullptr;
 };
 
@@ -674,6 +678,7 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->stream) (void)hipStreamSynchronize(g->stream);
         if (g->ws_ev_live) (void)hipEventSynchronize(g->ws_ev);
         if (g->ws_ev) (void)hipEventDestroy(g->ws_ev);
+        if (g->ssf_ev) (void)hipEventDestroy(g->ssf_ev);
         g->arena.release();
         g->flip_arena.release();
         g->lz_arena.release();
@@ -845,10 +850,17 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         size_t sb = 0;
         void* scr = message_scratch(G, p->method, p->precision, B, &sb);
         const hipStream_t s = (hipStream_t)stream;
+        const bool split = G->ssf_stream && G->ssf_stream != s && a.ssf;
+        if (split) {
+            a.ssf_stream = G->ssf_stream;
+            a.ssf_ev = G->ssf_ev;
+        }
         ws_acquire(G, s);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
-        ws_release(G, s);
+        // the last user of the queue is the SSF kernel: the workspace chain
+        // continues on its stream (the next decode on this handle waits for it)
+        ws_release(G, split ? G->ssf_stream : s);
     });
 }
 
@@ -976,6 +988,16 @@ int qd_osd_batch_device(qd_graph* G, int32_t method, int32_t order, int64_t B, c
         a.fail = fail;
         const int rc = launch_osd(G->dg, a, G->num_cus, (hipStream_t)stream);
         if (rc != 0) throw Fail(-104, std::string("osd launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
+int qd_graph_set_ssf_stream(qd_graph* G, void* ssf_stream) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        if (ssf_stream && !G->ssf_ev)
+            hip_check(hipEventCreateWithFlags(&G->ssf_ev, hipEventDisableTiming), "hipEventCreate");
+        G->ssf_stream = (hipStream_t)ssf_stream;
     });
 }
 

@@ -685,9 +685,16 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hip
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
     if (ssf_wave) {
-        rc = g.n_gen <= 64 ? launch_ssf_wave<1, RV, RC>(g, a, num_cus, stream)
-                           : launch_ssf_wave<2, RV, RC>(g, a, num_cus, stream);
-        record_ev(a, 2, stream);
+        hipStream_t ss = stream;
+        if (a.ssf_stream && a.ssf_stream != stream && a.ssf_ev) {  // SSF behind an event on its own stream
+            hipError_t e2 = hipEventRecord(a.ssf_ev, stream);
+            if (e2 == hipSuccess) e2 = hipStreamWaitEvent(a.ssf_stream, a.ssf_ev, 0);
+            if (e2 != hipSuccess) return (int)e2;
+            ss = a.ssf_stream;
+        }
+        rc = g.n_gen <= 64 ? launch_ssf_wave<1, RV, RC>(g, a, num_cus, ss)
+                           : launch_ssf_wave<2, RV, RC>(g, a, num_cus, ss);
+        record_ev(a, 2, ss);
         return rc;
     }
     rc = launch_ssf_block(g, a, num_cus, stream);

@@ -126,6 +126,11 @@ struct DecodeArgs {
     // min-sum wave kernel: counter of the dynamically scheduled shot chunks
     // (ShotSeq, qdec_bp_ms.h); zeroed by the launcher; nullptr -> static stride
     unsigned long long* wave_ctr;
+    // SSF on a second stream (qd_graph_set_ssf_stream, wave kernels only): the
+    // SSF kernel waits for ssf_ev (recorded after the BP kernel) on ssf_stream,
+    // so a later BP launch on the BP stream can overlap it; nullptr -> same stream
+    hipStream_t ssf_stream;
+    hipEvent_t ssf_ev;
     // optional timing (host side only): events recorded on the launch stream
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr

@@ -238,6 +238,13 @@ class Decoder:
             _abi.ptr(status), _abi.ptr(base), _abi.ptr(readout), _abi.ptr(osd0), _abi.ptr(osdw), _abi.ptr(corr),
             _abi.ptr(fail), C.c_void_p(stream)), "qd_osd_batch_device")
 
+    def set_ssf_stream(self, stream) -> None:
+        """Run the SSF kernel of later decode_device calls on `stream` (a torch
+        stream or a raw hipStream_t; None = the decode's own stream); see
+        qd_graph_set_ssf_stream: the caller synchronises with that stream."""
+        raw = None if stream is None else int(getattr(stream, "cuda_stream", stream))
+        _abi.check(self._lib.qd_graph_set_ssf_stream(self._handle, C.c_void_p(raw)), "qd_graph_set_ssf_stream")
+
     # ------------------------------------------------------------ timing
     def set_timing(self, capacity: int) -> None:
         """Record HIP events around the BP and SSF kernels of the next

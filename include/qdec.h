@@ -159,6 +159,16 @@ int qd_osd_batch_device(qd_graph* g, int32_t method, int32_t order, int64_t B, c
  * counterpart (the reference only reports whole-sweep walltime,
  * misc/p_sweep.py:26-33). */
 int qd_graph_set_timing(qd_graph* g, int32_t capacity);
+
+/* Route the SSF kernel of later qd_decode_batch_device calls (wave-kernel graphs)
+ * to `ssf_stream` (hipStream_t; NULL = the decode's own stream, the default):
+ * it runs behind an event recorded after the BP kernel on the decode stream, so
+ * a following BP launch on that stream overlaps it.  Outputs the SSF stage
+ * writes (status, ssf_steps, fail, x/corr of BP-failed shots) are complete when
+ * `ssf_stream` has passed that point; the caller synchronises with it.  The
+ * handle's next decode waits for this SSF kernel (workspace chain).  Replaces
+ * nothing in the reference (its decode is one synchronous call per shot). */
+int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
 
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out

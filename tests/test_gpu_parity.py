@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from conftest import load_checks
+from conftest import load_checks, load_code
 
 pytestmark = pytest.mark.gpu
 
@@ -284,3 +284,37 @@ def test_kernel_timing_ring(gpu_available, oracle_lib, code225):
     assert dec.read_timing()[0].shape == (0,)
     dec.set_timing(0)
     dec.decode(syn, readout=rd, want=("fail",))
+
+
+def test_ssf_stream_split_and_handle_chain(gpu_available, oracle_lib):
+    """qd_graph_set_ssf_stream: BP on one stream, SSF on another behind an event;
+    then two decodes on ONE handle enqueued on two different streams back to back
+    (the handle's workspace chain orders them).  Every output equals the oracle."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    dev = torch.device("cuda", 0)
+    p = 0.05
+    B = 3000
+    lz = np.asarray(load_code("hgp_12_3_4_s1234").logicals.z) % 2
+    syn, rd = oracle_lib.sample_storage(HZ, 0, p, p, seed=9, stream=0, shot0=0, B=2 * B)
+    ref = oracle_lib.decode(HZ, 2 * p / 3, syn, method="ms", precision="f64", max_iter=50, ssf=True, gens=HX,
+                            lz=lz, readout=rd, want_llr=False, ssf_impl="fast")
+    dec = Decoder(HZ, 2 * p / 3, method="ms", precision="f64", max_iter=50, flip_sets=HX, logicals=lz)
+    s1, s2, s3 = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = []
+    syn_d, rd_d = torch.from_numpy(syn).to(dev), torch.from_numpy(rd).to(dev)
+    for _ in range(2):
+        outs.append({k: torch.empty(B, dtype=dt, device=dev) for k, dt in
+                     (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32),
+                      ("fail", torch.uint8))})
+    torch.cuda.synchronize()  # inputs are on the device before the side streams read them
+    dec.set_ssf_stream(s3)
+    for h, st in ((0, s1), (1, s2)):
+        sl = slice(h * B, (h + 1) * B)
+        dec.decode_device(B, syn=syn_d[sl], readout=rd_d[sl], stream=st.cuda_stream, **outs[h])
+    torch.cuda.synchronize()
+    dec.set_ssf_stream(None)
+    for h in (0, 1):
+        sl = slice(h * B, (h + 1) * B)
+        for k in ("iters", "status", "ssf_steps", "fail"):
+            assert np.array_equal(outs[h][k].cpu().numpy(), ref[k][sl]), (h, k)
