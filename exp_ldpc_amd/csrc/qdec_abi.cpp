@@ -967,7 +967,7 @@ int qd_osd_batch_device(qd_graph* G, int32_t method, int32_t order, int64_t B, c
         if (B < 0) throw Fail(-8, "negative batch");
         if (!llr || (!syn && !syn_flags)) throw Fail(-83, "null OSD inputs");
         if (llr_precision != QD_F32 && llr_precision != QD_F64) throw Fail(-84, "invalid llr precision");
-        if (!osd_kernel_supports(G->dg)) throw Fail(-85, "graph too large for the device OSD (m <= 384, n < 1024)");
+        if (!osd_kernel_supports(G->dg)) throw Fail(-85, "graph too large for the device OSD (LDS image above 160 KiB)");
         if (fail && G->dg.k > 256) throw Fail(-86, "fused failure check after OSD supports <= 256 logicals");
         if (B == 0) return;
         set_device(G);

@@ -403,6 +403,324 @@ __global__ __launch_bounds__(64) void osd_wave_kernel(DevGraph g, OsdArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Workgroup variant for graphs beyond the register kernel (m > 384 or n >= 1024,
+// e.g. the R = 3 spacetime matrix 432 x 1224 of the reference's default bposd
+// mode): one 256-thread workgroup per BP-failed shot, the augmented rows
+// [H_sorted | s] in LDS as W 64-bit words each.  Same spec and tie rules as
+// osd_wave_kernel / the host stage (steps 1-6 above); the elimination walks the
+// sorted columns with the whole workgroup: block-wide first-row pivot search
+// (LDS atomic min), row swap, then the rows holding the pivot bit (flags taken
+// before any write) XOR the pivot row, over (row, word) pairs.  Candidate
+// weights are computed thread-parallel and the winner is the minimum of
+// (weight, position in the host's candidate order).
+constexpr int kOsdBlock = 256;
+
+struct OsdBlockLayout {
+    int ns, W, RW, o_rows, o_key, o_idx, o_pos, o_piv, o_npv, o_isp, o_out, o_hit, o_x0, o_tcl, o_ctl, total;
+    __host__ __device__ OsdBlockLayout(int n, int m) {
+        ns = 64;
+        while (ns < n) ns <<= 1;
+        W = (n + 1 + 63) / 64;
+        RW = (m + 63) / 64;
+        int o = 0;
+        auto take = [&](int bytes) {
+            const int at = o;
+            o += (bytes + 15) / 16 * 16;
+            return at;
+        };
+        o_rows = take(8 * m * W);
+        o_key = take(8 * ns);
+        o_x0 = take(8 * RW);
+        o_tcl = take(8 * kOsdMaxLam * RW);
+        o_ctl = take(64);
+        o_idx = take(2 * ns);
+        o_pos = take(2 * n);
+        o_piv = take(2 * (m > 0 ? m : 1));
+        o_npv = take(2 * n);
+        o_isp = take(n);
+        o_out = take(n);
+        o_hit = take(m);
+        total = o;
+    }
+};
+
+__global__ __launch_bounds__(kOsdBlock) void osd_block_kernel(DevGraph g, OsdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = g.m, n = g.n;
+    const OsdBlockLayout L(n, m);
+    const int W = L.W, RW = L.RW, NS = L.ns;
+    uint64_t* A = reinterpret_cast<uint64_t*>(smem + L.o_rows);       // [m][W]
+    uint64_t* skey = reinterpret_cast<uint64_t*>(smem + L.o_key);
+    uint64_t* x0 = reinterpret_cast<uint64_t*>(smem + L.o_x0);        // [RW] transformed syndrome over pivot rows
+    uint64_t* tcl = reinterpret_cast<uint64_t*>(smem + L.o_tcl);      // [lam][RW] transformed columns
+    unsigned long long* ctl = reinterpret_cast<unsigned long long*>(smem + L.o_ctl);  // [0] pivot, [1] best key
+    uint16_t* sidx = reinterpret_cast<uint16_t*>(smem + L.o_idx);
+    uint16_t* pos = reinterpret_cast<uint16_t*>(smem + L.o_pos);
+    uint16_t* pivc = reinterpret_cast<uint16_t*>(smem + L.o_piv);
+    uint16_t* npv = reinterpret_cast<uint16_t*>(smem + L.o_npv);
+    uint8_t* isp = smem + L.o_isp;
+    uint8_t* outb = smem + L.o_out;
+    uint8_t* hit = smem + L.o_hit;
+    const int32_t* rp = g.row_ptr;
+    const int32_t* ci = g.col_idx;
+    auto bit = [&](int i, int k) -> int { return (int)((A[(size_t)i * W + (k >> 6)] >> (k & 63)) & 1); };
+
+    for (int64_t shot = blockIdx.x; shot < a.B; shot += gridDim.x) {
+        if (a.status && (a.status[shot] & 1)) continue;  // uniform over the workgroup
+        // ---- 1. stable sort of the columns by log-probability ratio
+        for (int k = tid; k < NS; k += kOsdBlock) {
+            uint64_t key = ~0ull;
+            uint16_t idx = 0xffff;
+            if (k < n) {
+                const double v = a.llr_f32 ? (double)static_cast<const float*>(a.llr)[shot * n + k]
+                                           : static_cast<const double*>(a.llr)[shot * n + k];
+                key = order_key(v);
+                idx = (uint16_t)k;
+            }
+            skey[k] = key;
+            sidx[k] = idx;
+        }
+        __syncthreads();
+        for (int size = 2; size <= NS; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int t = tid; t < NS / 2; t += kOsdBlock) {
+                    const int i = 2 * t - (t & (stride - 1));
+                    const int j = i + stride;
+                    const uint64_t ki = skey[i], kj = skey[j];
+                    const uint16_t ii = sidx[i], ij = sidx[j];
+                    const bool gt = ki > kj || (ki == kj && ii > ij);
+                    if (gt == ((i & size) == 0)) {
+                        skey[i] = kj;
+                        skey[j] = ki;
+                        sidx[i] = ij;
+                        sidx[j] = ii;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int k = tid; k < n; k += kOsdBlock) {
+            pos[sidx[k]] = (uint16_t)k;
+            isp[k] = 0;
+        }
+        for (int e = tid; e < m * W; e += kOsdBlock) A[e] = 0;
+        __syncthreads();
+
+        // ---- 2. augmented rows [H_sorted | s] (one thread per row)
+        for (int i = tid; i < m; i += kOsdBlock) {
+            uint64_t* r = A + (size_t)i * W;
+            int sb = a.syn ? (a.syn[shot * m + i] & 1) : 0;
+            for (int e = rp[i]; e < rp[i + 1]; ++e) {
+                const int j = ci[e];
+                const int k = pos[j];
+                r[k >> 6] ^= 1ull << (k & 63);
+                if (a.syn_flags && j < g.n_data) {
+                    if ((a.syn_flags & 1) && a.base) sb ^= a.base[shot * g.n_data + j] & 1;
+                    if ((a.syn_flags & 2) && a.readout) sb ^= a.readout[shot * g.n_data + j] & 1;
+                }
+            }
+            if (sb) r[n >> 6] ^= 1ull << (n & 63);
+        }
+        __syncthreads();
+
+        // ---- 3. Gauss-Jordan in sorted column order
+        int rank = 0;
+        for (int k = 0; k < n && rank < m; ++k) {
+            if (tid == 0) ctl[0] = ~0ull;
+            __syncthreads();
+            unsigned long long cand = ~0ull;
+            for (int i = rank + tid; i < m; i += kOsdBlock)
+                if (bit(i, k)) {
+                    cand = (unsigned long long)i;
+                    break;
+                }
+            if (cand != ~0ull) atomicMin(&ctl[0], cand);
+            __syncthreads();
+            const unsigned long long pv = ctl[0];
+            if (pv == ~0ull) continue;  // uniform
+            const int piv = (int)pv, ww = k >> 6;
+            if (piv != rank)
+                for (int w = ww + tid; w < W; w += kOsdBlock) {
+                    const uint64_t t = A[(size_t)piv * W + w];
+                    A[(size_t)piv * W + w] = A[(size_t)rank * W + w];
+                    A[(size_t)rank * W + w] = t;
+                }
+            for (int i = tid; i < m; i += kOsdBlock) hit[i] = (uint8_t)(i != rank && i != piv && bit(i, k));
+            __syncthreads();
+            if (tid == 0) hit[piv] = (uint8_t)(piv != rank && bit(piv, k));  // the swapped-out row
+            __syncthreads();
+            const int nw = W - ww;
+            for (int e = tid; e < m * nw; e += kOsdBlock) {
+                const int i = e / nw, w = ww + e % nw;
+                if (hit[i]) A[(size_t)i * W + w] ^= A[(size_t)rank * W + w];
+            }
+            if (tid == 0) {
+                pivc[rank] = (uint16_t)k;
+                isp[k] = 1;
+            }
+            ++rank;
+            __syncthreads();
+        }
+
+        // ---- 4. transformed syndrome, non-pivot columns, the first lam transformed columns
+        for (int w = tid; w < RW; w += kOsdBlock) {
+            uint64_t v = 0;
+            for (int b = 0; b < 64; ++b) {
+                const int i = w * 64 + b;
+                if (i < rank && bit(i, n)) v |= 1ull << b;
+            }
+            x0[w] = v;
+        }
+        if (wave == 0) {
+            int kn = 0;
+            for (int base = 0; base < n; base += 64) {
+                const int k = base + lane;
+                const bool f = k < n && !isp[k];
+                const uint64_t bal = __ballot(f);
+                if (f) npv[kn + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;
+                kn += __popcll(bal);
+            }
+            if (lane == 0) ctl[2] = (unsigned long long)kn;
+        }
+        __syncthreads();
+        const int kn = (int)ctl[2];
+        const int lam = a.order < 0 ? 0 : (a.order < kn ? a.order : kn);
+        const int lam_s = lam < kOsdMaxLam ? lam : kOsdMaxLam;
+        for (int e = tid; e < lam_s * RW; e += kOsdBlock) {
+            const int t = e / RW, w = e % RW, k = npv[t];
+            uint64_t v = 0;
+            for (int b = 0; b < 64; ++b) {
+                const int i = w * 64 + b;
+                if (i < rank && bit(i, k)) v |= 1ull << b;
+            }
+            tcl[t * RW + w] = v;
+        }
+        int w0 = 0;
+        for (int w = 0; w < RW; ++w) w0 += __popcll(x0[w]);
+        if (tid == 0) ctl[1] = ((unsigned long long)w0 << 32);  // OSD-0: weight, order 0
+        __syncthreads();
+
+        // ---- 5. candidates: key = weight << 32 | position in the host's order
+        // (1 + t: single t, 1 + kn + pair index, or the OSD-E mask)
+        unsigned long long best = ~0ull;
+        if (a.method == 2) {
+            for (int t = tid; t < kn; t += kOsdBlock) {
+                const int k = npv[t];
+                int wgt = 1;
+                for (int w = 0; w < RW; ++w) {
+                    uint64_t v = 0;
+                    for (int b = 0; b < 64; ++b) {
+                        const int i = w * 64 + b;
+                        if (i < rank && bit(i, k)) v |= 1ull << b;
+                    }
+                    wgt += __popcll(x0[w] ^ v);
+                }
+                const unsigned long long key = ((unsigned long long)wgt << 32) | (unsigned long long)(1 + t);
+                best = key < best ? key : best;
+            }
+            const int np = lam_s * (lam_s - 1) / 2;
+            for (int q = tid; q < np; q += kOsdBlock) {
+                int u = 0, rem = q;  // q -> (u, v), u < v, lexicographic
+                while (rem >= lam_s - 1 - u) {
+                    rem -= lam_s - 1 - u;
+                    ++u;
+                }
+                const int v = u + 1 + rem;
+                int wgt = 2;
+                for (int w = 0; w < RW; ++w) wgt += __popcll(x0[w] ^ tcl[u * RW + w] ^ tcl[v * RW + w]);
+                const unsigned long long key = ((unsigned long long)wgt << 32) | (unsigned long long)(1 + kn + q);
+                best = key < best ? key : best;
+            }
+        } else if (a.method == 1 && lam_s > 0) {
+            const uint32_t lim = 1u << lam_s;
+            for (uint32_t sm = 1 + tid; sm < lim; sm += kOsdBlock) {
+                int wgt = __popc(sm);
+                for (int w = 0; w < RW; ++w) {
+                    uint64_t c = x0[w];
+                    for (int t = 0; t < lam_s; ++t)
+                        if ((sm >> t) & 1) c ^= tcl[t * RW + w];
+                    wgt += __popcll(c);
+                }
+                const unsigned long long key = ((unsigned long long)wgt << 32) | sm;
+                best = key < best ? key : best;
+            }
+        }
+        // OSD-0 keeps a tie (strict improvement): its key has the lowest position
+        if (best != ~0ull) atomicMin(&ctl[1], best);
+        __syncthreads();
+        const unsigned long long bk = ctl[1];
+        const int bpos = (int)(bk & 0xffffffffu);
+        int kind = 0, ca = -1, cb = -1;
+        uint32_t cmask = 0;
+        if (bpos != 0) {
+            if (a.method == 2) {
+                if (bpos <= kn) {
+                    kind = 1;
+                    ca = bpos - 1;
+                } else {
+                    int q = bpos - 1 - kn, u = 0;
+                    while (q >= lam_s - 1 - u) {
+                        q -= lam_s - 1 - u;
+                        ++u;
+                    }
+                    kind = 2;
+                    ca = u;
+                    cb = u + 1 + q;
+                }
+            } else {
+                kind = 3;
+                cmask = (uint32_t)bpos;
+            }
+        }
+
+        // ---- 6. outputs (osd0, then the chosen candidate + fused fold / failure check)
+        auto emit = [&](int kd) {
+            for (int j = tid; j < n; j += kOsdBlock) outb[j] = 0;
+            __syncthreads();
+            for (int i = tid; i < rank; i += kOsdBlock) {
+                int xb = (int)((x0[i >> 6] >> (i & 63)) & 1);
+                if (kd == 1) xb ^= bit(i, npv[ca]);
+                if (kd == 2) xb ^= (int)(((tcl[ca * RW + (i >> 6)] ^ tcl[cb * RW + (i >> 6)]) >> (i & 63)) & 1);
+                if (kd == 3)
+                    for (int t = 0; t < lam_s; ++t)
+                        if ((cmask >> t) & 1) xb ^= (int)((tcl[t * RW + (i >> 6)] >> (i & 63)) & 1);
+                if (xb) outb[sidx[pivc[i]]] = 1;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (kd == 1) outb[sidx[npv[ca]]] ^= 1;
+                if (kd == 2) {
+                    outb[sidx[npv[ca]]] ^= 1;
+                    outb[sidx[npv[cb]]] ^= 1;
+                }
+                if (kd == 3)
+                    for (int t = 0; t < lam_s; ++t)
+                        if ((cmask >> t) & 1) outb[sidx[npv[t]]] ^= 1;
+            }
+            __syncthreads();
+        };
+        if (a.osd0_out) {
+            emit(0);
+            for (int j = tid; j < n; j += kOsdBlock) a.osd0_out[shot * n + j] = outb[j];
+            __syncthreads();
+        }
+        emit(kind);
+        if (wave == 0) {
+            DecodeArgs fa{};
+            fa.B = a.B;
+            fa.base = a.base;
+            fa.readout = a.readout;
+            fa.x_out = a.osdw_out;
+            fa.corr_out = a.corr_out;
+            fa.fail = a.fail;
+            finalize_shot(g, fa, shot, outb, false, false, 0, lane);
+        }
+        __syncthreads();
+    }
+}
+
 namespace {
 template <int RS, int W>
 int launch_osd_shape(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream_t stream) {
@@ -423,7 +741,7 @@ int launch_osd_shape(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream
 
 static int osd_row_slots(int m) { return m <= 128 ? 2 : (m <= 256 ? 4 : 6); }
 
-bool osd_kernel_supports(const DevGraph& g) {
+static bool osd_wave_supports(const DevGraph& g) {
     if (g.m <= 0 || g.m > 384 || g.n + 1 > 1024) return false;
     const int rs = osd_row_slots(g.m);
     const int need = (g.n + 1 + 63) / 64;
@@ -433,9 +751,31 @@ bool osd_kernel_supports(const DevGraph& g) {
     return false;
 }
 
+// the workgroup variant: its LDS image within one CU's 160 KiB, 16-bit indices
+static bool osd_block_supports(const DevGraph& g) {
+    if (g.m <= 0 || g.n <= 0 || g.n >= 65535 || g.m >= 65535) return false;
+    return OsdBlockLayout(g.n, g.m).total <= 160 * 1024 && g.k <= 256;
+}
+
+bool osd_kernel_supports(const DevGraph& g) { return osd_wave_supports(g) || osd_block_supports(g); }
+
 int launch_osd(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream_t stream) {
     if (a.B <= 0) return 0;
-    if (!osd_kernel_supports(g)) return (int)hipErrorNotSupported;
+    if (!osd_wave_supports(g)) {
+        if (!osd_block_supports(g)) return (int)hipErrorNotSupported;
+        const OsdBlockLayout L(g.n, g.m);
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&osd_block_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, L.total);
+        if (e != hipSuccess) return (int)e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, osd_block_kernel, kOsdBlock, L.total);
+        if (e != hipSuccess) return (int)e;
+        if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+        long long grid = (long long)num_cus * per_cu;
+        if (grid > a.B) grid = a.B;
+        hipLaunchKernelGGL(osd_block_kernel, dim3((unsigned)grid), dim3(kOsdBlock), L.total, stream, g, a);
+        return (int)hipGetLastError();
+    }
     const int rs = osd_row_slots(g.m);
     const int need = (g.n + 1 + 63) / 64;
 #define QDEC_OSD_LAUNCH(R, V) \

@@ -26,6 +26,9 @@ def _graphs():
         "R0": sp.csr_matrix(HZ),
         "R1": sp.csr_matrix(SpacetimeCode(HZ, 1).spacetime_check_matrix),
         "R2": sp.csr_matrix(SpacetimeCode(HZ, 2).spacetime_check_matrix),
+        # beyond the register kernel (m > 384, n >= 1024): workgroup kernel, rows in LDS
+        "R3": sp.csr_matrix(SpacetimeCode(HZ, 3).spacetime_check_matrix),
+        "R4": sp.csr_matrix(SpacetimeCode(HZ, 4).spacetime_check_matrix),
         "single_shot": sp.csr_matrix(SpacetimeCodeSingleShot(HZ).spacetime_check_matrix),
         "ragged": make_check_matrix(rows, n),
     }
@@ -96,7 +99,8 @@ def test_device_osd_matches_numpy_checker(gpu_available):
         assert ((H @ ow_h[b]) % 2 == syn[b]).all() or not ((H @ rw) % 2 == syn[b]).all()
 
 
-@pytest.mark.parametrize("mode,rounds", [("bposd", 1), ("bposd", 0), ("bposd_hybrid", 1), ("bposd_single_shot", 2)])
+@pytest.mark.parametrize("mode,rounds", [("bposd", 1), ("bposd", 0), ("bposd", 3), ("bposd_hybrid", 1),
+                                         ("bposd_single_shot", 2)])
 def test_pipeline_device_osd_equals_host_osd(gpu_available, mode, rounds):
     """The batched pipeline with the device OSD returns the same corrections and
     failure flags as with the host OSD stage (forced by hiding device support)."""
@@ -120,3 +124,36 @@ def test_pipeline_device_osd_equals_host_osd(gpu_available, mode, rounds):
     assert np.array_equal(dev_res.corrections, host_res.corrections)
     assert np.array_equal(dev_res.fail, host_res.fail)
     assert dev_res.bp_converged < 2000
+
+
+@pytest.mark.parametrize("gname", ["R3", "R4"])
+def test_device_osd_block_matches_numpy_checker(gpu_available, gname):
+    """The workgroup OSD kernel (R = 3 / 4 spacetime matrices, rows in LDS)
+    against the independent numpy restatement, osd_cs order 7 and osd_e 4."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    from oracle.osd_py import osd_decode
+    H = GRAPHS[gname]
+    m, n = H.shape
+    assert m > 384 and n >= 1024
+    rng = np.random.default_rng(13)
+    B = 6
+    e = (rng.random((B, n)) < 0.03).astype(np.uint8)
+    syn = np.ascontiguousarray((H @ e.T).T % 2, dtype=np.uint8)
+    dec = Decoder(H, 0.02, method="ms", precision="f32", max_iter=2)
+    assert dec.osd_device_supported
+    dev = torch.device("cuda", 0)
+    syn_d = torch.from_numpy(syn).to(dev)
+    llr = torch.empty((B, n), dtype=torch.float32, device=dev)
+    dec.decode_device(B, syn=syn_d, llr=llr)
+    for method, order in (("osd_cs", 7), ("osd_e", 4)):
+        o0 = torch.zeros((B, n), dtype=torch.uint8, device=dev)
+        ow = torch.zeros((B, n), dtype=torch.uint8, device=dev)
+        dec.osd_device(B, llr=llr, method=method, order=order, syn=syn_d, osd0=o0, osdw=ow)
+        torch.cuda.synchronize()
+        llr_h = llr.cpu().numpy().astype(np.float64)
+        for b in range(B):
+            r0, rw = osd_decode(H, syn[b], llr_h[b], method, order)
+            assert np.array_equal(o0.cpu().numpy()[b], r0), (method, b)
+            assert np.array_equal(ow.cpu().numpy()[b], rw), (method, b)
+            assert ((H @ rw) % 2 == syn[b]).all()
