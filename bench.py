@@ -14,7 +14,8 @@ f32 (the stated-tolerance variant) and reported under `variants`.
 
 Phases (rank 0 prints ONE JSON line):
   1. headline: W warmup + K timed steps, the 9 points round-robin over --streams
-     HIP streams, so kernels of independent points fill each other's tails
+     HIP streams (default 9: every point on its own stream; measured 79 vs 76 M
+     f64 shots/s at 5), so kernels of independent points fill each other's tails
      (--schedule pipeline: every BP kernel on one stream and every SSF kernel on
      a second one behind an event -- measured slower: the persistent BP kernel
      fills every CU, so SSF only runs in BP's tail, which it cannot fill because
@@ -305,7 +306,7 @@ def main():
                     help="second precision decoded on the same shots (reported under variants)")
     ap.add_argument("--cpu-shots", type=int, default=200000, help="CPU-baseline shots per sweep point")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=5, help="HIP streams the sweep points are spread over "
+    ap.add_argument("--streams", type=int, default=9, help="HIP streams the sweep points are spread over "
                                                            "(--schedule streams)")
     ap.add_argument("--schedule", default="streams", choices=["pipeline", "streams"],
                     help="pipeline: every BP kernel on one stream, every SSF kernel on a second one behind an "
