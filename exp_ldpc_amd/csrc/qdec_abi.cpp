@@ -605,6 +605,8 @@ DecodeArgs make_args(const qd_graph* g, const qd_params* p, int64_t B, const uin
     if (!syn && !(a.syn_flags && (base || readout))) throw Fail(-7, "no syndrome source");
     if (!g->ctl) hip_check(hipMalloc(&const_cast<qd_graph*>(g)->ctl, 256), "hipMalloc control block");
     a.wave_ctr = static_cast<unsigned long long*>(g->ctl);
+    const char* ns = std::getenv("QDEC_SSF_NOSPLIT");
+    a.ssf_nosplit = (ns && ns[0] == '1') ? 1 : 0;
     return a;
 }
 
@@ -843,6 +845,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         check_graph(G);
         check_params(G, p);
         if (B < 0) throw Fail(-8, "negative batch");
+        if (B == 0) return;  // nothing to enqueue
         set_device(G);
         DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
         attach_queue(G, a, p->method, p->precision);
@@ -936,7 +939,9 @@ int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double 
                              void* stream) {
     return guarded([&] {
         check_graph(G);
-        if (rounds < 0 || B < 0 || !syn || !readout) throw Fail(-60, "invalid sampler arguments");
+        if (rounds < 0 || B < 0) throw Fail(-60, "invalid sampler arguments");
+        if (B == 0) return;
+        if (!syn || !readout) throw Fail(-60, "invalid sampler arguments");
         if (G->dg.fold_blocks != 1 || G->dg.n_data != G->dg.n) throw Fail(-61, "sampler needs a plain code graph (H = Hz)");
         auto thr = [](double p) -> uint32_t {
             if (!(p > 0)) return 0u;
@@ -965,6 +970,7 @@ int qd_osd_batch_device(qd_graph* G, int32_t method, int32_t order, int64_t B, c
         if (method == 1 && order > 20) throw Fail(-81, "osd_e order above 20 is not supported");
         if (method == 2 && order > 64) throw Fail(-82, "osd_cs order above 64 is not supported on the device");
         if (B < 0) throw Fail(-8, "negative batch");
+        if (B == 0) return;
         if (!llr || (!syn && !syn_flags)) throw Fail(-83, "null OSD inputs");
         if (llr_precision != QD_F32 && llr_precision != QD_F64) throw Fail(-84, "invalid llr precision");
         if (!osd_kernel_supports(G->dg)) throw Fail(-85, "graph too large for the device OSD (LDS image above 160 KiB)");

@@ -387,6 +387,9 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
     const bool lean_fin = !a.x_out && !a.corr_out && !a.base && g.fold_blocks == 1;
     const bool want_fail = a.fail && a.readout && g.k > 0;
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
+    // the split scorer enumerates hi < 8 per lane (generators of up to 8 qubits
+    // have nhi <= 16, half <= 8); QDEC_SSF_NOSPLIT=1 at launch disables it
+    const bool split_ok = nhi <= 16 && !a.ssf_nosplit;
     const int nlcw = (g.g_nlcmax + 3) / 4;
     QDEC_STAMP_DECL
     const int slot0 = blockIdx.x * kSsfWaves + wave;
@@ -464,7 +467,26 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             wave_lds_sync();
             QDEC_STAMP(0);
             QDEC_COUNT(5, nl);
-            // ---- 2. score the listed generators ----
+            // ---- 2. score the listed generators (<= 32 listed and >= 5 qubits:
+            // two lanes per generator, each half of its subsets) ----
+            if (nl <= 32 && nhi >= 2 && split_ok) {
+                const int idx = lane & 31;
+                const bool upper = lane >= 32;
+                uint32_t sl = 0, qm[kGenW];
+                int gg = 0;
+                if (idx < nl) {
+                    gg = list[idx];
+                    sl = slt[idx];
+                }
+#pragma unroll
+                for (int k = 0; k < kGenW; ++k) qm[k] = idx < nl ? qmt[k * GP + gg] : 0u;
+                uint32_t top = 0;
+#pragma unroll
+                for (int k = 0; k < kGenW; ++k)
+                    if (k == g.g_wmax - 1) top = qm[k];
+                const int sc = gen_best_score_split(sl, qm, nhi / 2, top, upper);
+                if (!upper && idx < nl) key[gg] = (int)(((unsigned)sc << 15) | ((unsigned)(127 - gg) << 8));
+            } else
             for (int c0 = 0; c0 < nl; c0 += 64) {
                 const int idx = c0 + lane;
                 if (idx < nl) {
@@ -496,14 +518,14 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             // lane k < kGenW holds qubit k's mask of the chosen generator
             const uint32_t qk = lane < kGenW ? qmt[lane * GP + gsel] : 0u;
             int tsel = -1;
+            uint32_t qs[kGenW];  // the chosen generator's qubit masks, broadcast once
+#pragma unroll
+            for (int k = 0; k < kGenW; ++k) qs[k] = (uint32_t)__builtin_amdgcn_readlane((int)qk, k);
             for (int t0 = 0; t0 < 16 * nhi; t0 += 64) {
                 const int t = t0 + lane;
                 uint32_t mt = 0;
 #pragma unroll
-                for (int k = 0; k < kGenW; ++k) {
-                    const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)qk, k);
-                    mt ^= ((t >> k) & 1) ? q : 0u;
-                }
+                for (int k = 0; k < kGenW; ++k) mt ^= ((t >> k) & 1) ? qs[k] : 0u;
                 const int gain = base - __builtin_popcount(slg ^ mt);
                 const bool hit = t > 0 && t < 16 * nhi && gain * kSsfScale == score * __builtin_popcount(t);
                 const unsigned long long hb = __ballot(hit);

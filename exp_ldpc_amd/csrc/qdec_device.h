@@ -219,6 +219,54 @@ __device__ __forceinline__ int gen_best_score(uint32_t sl, const uint32_t (&qm)[
     return best;
 }
 
+// Half of a generator's subsets, for listing steps with <= 32 generators: lane
+// l < 32 takes the subsets without the generator's last qubit (hi < half),
+// lane l + 32 those with it (hi + half); the partners' per-size minima are
+// combined by lane-xor-32 shuffles, and lane l gets the same score as
+// gen_best_score (the minima are over the same subsets).  `top` = the mask of
+// the last qubit (index wmax - 1), half = nhi / 2 >= 1.
+__device__ __forceinline__ int gen_best_score_split(uint32_t sl, const uint32_t (&qm)[kGenW], int half,
+                                                    uint32_t top, bool upper) {
+    const int base = __builtin_popcount(sl);
+    uint32_t lo[16];
+    lo[0] = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
+    uint32_t mn[kGenW + 1];
+#pragma unroll
+    for (int d = 0; d <= kGenW; ++d) mn[d] = 64u;
+    const uint32_t extra = upper ? top : 0u;
+#pragma unroll
+    for (int hh = 0; hh < 8; ++hh) {
+        if (hh < half) {  // uniform
+            uint32_t mh = extra;
+#pragma unroll
+            for (int bb = 0; bb < 3; ++bb)
+                if ((hh >> bb) & 1) mh ^= qm[4 + bb];
+            const uint32_t sh = sl ^ mh;
+#pragma unroll
+            for (int l = 0; l < 16; ++l) {
+                // dd = subset size without the last qubit; the upper lane's size is dd + 1
+                const int dd = __builtin_popcount(hh) + __builtin_popcount(l);
+                uint32_t pc = (uint32_t)__builtin_popcount(sh ^ lo[l]);
+                if (hh == 0 && l == 0) pc = upper ? pc : 64u;  // the empty set (lower lane only)
+                mn[dd] = min(mn[dd], pc);
+            }
+        }
+    }
+    // partner's minima: upper lanes hold sizes dd + 1 at index dd
+    uint32_t other[kGenW + 1];
+#pragma unroll
+    for (int d = 0; d <= kGenW; ++d) other[d] = (uint32_t)__shfl_xor((int)mn[d], 32);
+    int best = INT_MIN;
+#pragma unroll
+    for (int d = 1; d <= kGenW; ++d) {
+        const uint32_t m2 = min(mn[d], other[d - 1]);  // lower lane: own size d, partner's size (d-1)+1
+        best = max(best, (base - (int)m2) * (840 / d));
+    }
+    return best;
+}
+
 // (score, -g, -t) packed so that a signed max picks the spec's winner.
 __device__ __forceinline__ long long gen_key64(int best32, int gi) {
     return ((long long)(best32 >> 8) << 32) | ((long long)(0xFFFFFF - gi) << 8) | (long long)(best32 & 255);

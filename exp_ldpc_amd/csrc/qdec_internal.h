@@ -131,6 +131,9 @@ struct DecodeArgs {
     // so a later BP launch on the BP stream can overlap it; nullptr -> same stream
     hipStream_t ssf_stream;
     hipEvent_t ssf_ev;
+    // SSF wave kernel: 1 disables the two-lanes-per-generator scoring of short
+    // listing steps (QDEC_SSF_NOSPLIT=1; parity tests run both ways)
+    int ssf_nosplit;
     // optional timing (host side only): events recorded on the launch stream
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr

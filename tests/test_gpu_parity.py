@@ -62,14 +62,18 @@ def test_bp_parity(gpu_available, oracle_lib, method, precision, shape):
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("max_iter", [1, 3, 50])
-@pytest.mark.parametrize("local_syndromes", ["incremental", "gather"])
+@pytest.mark.parametrize("local_syndromes", ["incremental", "gather", "nosplit"])
 def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, local_syndromes, code225, monkeypatch):
     """Both ways the wave SSF kernel keeps generator-local syndromes: updated
     through the check -> generator table after each flip (default), or
-    re-gathered from the residual every step (QDEC_SSF_GATHER=1)."""
+    re-gathered from the residual every step (QDEC_SSF_GATHER=1); and with the
+    two-lanes-per-generator scoring of short listing steps off
+    (QDEC_SSF_NOSPLIT=1)."""
     from exp_ldpc_amd.decoder import Decoder
     if local_syndromes == "gather":
         monkeypatch.setenv("QDEC_SSF_GATHER", "1")
+    if local_syndromes == "nosplit":
+        monkeypatch.setenv("QDEC_SSF_NOSPLIT", "1")
     rng = np.random.default_rng(max_iter)
     B = 2000
     rd = _errors(rng, B, 225, 0.03)
@@ -318,3 +322,29 @@ def test_ssf_stream_split_and_handle_chain(gpu_available, oracle_lib):
         sl = slice(h * B, (h + 1) * B)
         for k in ("iters", "status", "ssf_steps", "fail"):
             assert np.array_equal(outs[h][k].cpu().numpy(), ref[k][sl]), (h, k)
+
+
+def test_empty_batch_and_buffer_validation(gpu_available):
+    """B = 0 is a no-op on every entry point; mistyped or short device buffers
+    are rejected in Python before any launch (no out-of-bounds device access)."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    dev = torch.device("cuda", 0)
+    dec = Decoder(HZ, 0.01, method="ms", precision="f64", max_iter=10, flip_sets=HX)
+    out = dec.decode(np.zeros((0, HZ.shape[0]), np.uint8))
+    assert out["x"].shape == (0, HZ.shape[1]) and out["fail"].shape == (0,)
+    e = torch.empty((0, HZ.shape[0]), dtype=torch.uint8, device=dev)
+    dec.decode_device(0, syn=e, iters=torch.empty(0, dtype=torch.int32, device=dev))
+    dec.sample_storage_device(0, 0.01, 0.01, 1, 0, 0, 0, e, torch.empty((0, HZ.shape[1]), dtype=torch.uint8,
+                                                                         device=dev))
+    llr = torch.empty((0, HZ.shape[1]), dtype=torch.float64, device=dev)
+    dec.osd_device(0, llr=llr, method="osd_cs", order=7, syn=e)
+    torch.cuda.synchronize()
+    B = 8
+    syn = torch.zeros((B, HZ.shape[0]), dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):  # f32 llr buffer for an f64 decoder
+        dec.decode_device(B, syn=syn, llr=torch.empty((B, HZ.shape[1]), dtype=torch.float32, device=dev))
+    with pytest.raises(ValueError):  # too short
+        dec.decode_device(B, syn=syn[:4])
+    with pytest.raises(ValueError):  # host tensor
+        dec.decode_device(B, syn=syn.cpu())
