@@ -470,8 +470,10 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             // ---- 2. score the listed generators (<= 32 listed and >= 5 qubits:
             // two lanes per generator, each half of its subsets) ----
             if (nl <= 32 && nhi >= 2 && split_ok) {
-                const int idx = lane & 31;
-                const bool upper = lane >= 32;
+                const bool four = nl <= 16 && nhi >= 4;
+                const int sw = four ? 16 : 32;
+                const int idx = lane & (sw - 1);
+                const int q = lane / sw;
                 uint32_t sl = 0, qm[kGenW];
                 int gg = 0;
                 if (idx < nl) {
@@ -480,12 +482,15 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
                 }
 #pragma unroll
                 for (int k = 0; k < kGenW; ++k) qm[k] = idx < nl ? qmt[k * GP + gg] : 0u;
-                uint32_t top = 0;
+                uint32_t tq[2] = {0u, 0u};  // the generator's last two qubit masks (wmax-1, wmax-2)
 #pragma unroll
-                for (int k = 0; k < kGenW; ++k)
-                    if (k == g.g_wmax - 1) top = qm[k];
-                const int sc = gen_best_score_split(sl, qm, nhi / 2, top, upper);
-                if (!upper && idx < nl) key[gg] = (int)(((unsigned)sc << 15) | ((unsigned)(127 - gg) << 8));
+                for (int k = 0; k < kGenW; ++k) {
+                    if (k == g.g_wmax - 1) tq[0] = qm[k];
+                    if (k == g.g_wmax - 2) tq[1] = qm[k];
+                }
+                const int sc = four ? gen_best_score_split<4>(sl, qm, nhi / 4, tq, q)
+                                    : gen_best_score_split<2>(sl, qm, nhi / 2, tq, q);
+                if (q == 0 && idx < nl) key[gg] = (int)(((unsigned)sc << 15) | ((unsigned)(127 - gg) << 8));
             } else
             for (int c0 = 0; c0 < nl; c0 += 64) {
                 const int idx = c0 + lane;

@@ -219,14 +219,17 @@ __device__ __forceinline__ int gen_best_score(uint32_t sl, const uint32_t (&qm)[
     return best;
 }
 
-// Half of a generator's subsets, for listing steps with <= 32 generators: lane
-// l < 32 takes the subsets without the generator's last qubit (hi < half),
-// lane l + 32 those with it (hi + half); the partners' per-size minima are
-// combined by lane-xor-32 shuffles, and lane l gets the same score as
-// gen_best_score (the minima are over the same subsets).  `top` = the mask of
-// the last qubit (index wmax - 1), half = nhi / 2 >= 1.
-__device__ __forceinline__ int gen_best_score_split(uint32_t sl, const uint32_t (&qm)[kGenW], int half,
-                                                    uint32_t top, bool upper) {
+// A 1/S share of a generator's subsets (S = 2 or 4), for listing steps with
+// <= 64/S generators: the S lanes l + (64/S) q, q < S, score the same generator,
+// lane q taking the subsets whose top log2(S) qubits (the generator's last ones)
+// are the bits of q.  Per-size minima are then combined by lane-xor shuffles
+// and lane q = 0 gets the same score as gen_best_score (the minima are over the
+// same subsets).  tq = masks of those top qubits (tq[0] the highest),
+// part = nhi / S >= 1 hi values per lane.
+template <int S>
+__device__ __forceinline__ int gen_best_score_split(uint32_t sl, const uint32_t (&qm)[kGenW], int part,
+                                                    const uint32_t (&tq)[2], int q) {
+    static_assert(S == 2 || S == 4, "split");
     const int base = __builtin_popcount(sl);
     uint32_t lo[16];
     lo[0] = 0;
@@ -235,10 +238,11 @@ __device__ __forceinline__ int gen_best_score_split(uint32_t sl, const uint32_t 
     uint32_t mn[kGenW + 1];
 #pragma unroll
     for (int d = 0; d <= kGenW; ++d) mn[d] = 64u;
-    const uint32_t extra = upper ? top : 0u;
+    // q's bit 0 selects the highest qubit, bit 1 (S = 4) the next one
+    const uint32_t extra = ((q & 1) ? tq[0] : 0u) ^ ((S == 4 && (q & 2)) ? tq[1] : 0u);
 #pragma unroll
     for (int hh = 0; hh < 8; ++hh) {
-        if (hh < half) {  // uniform
+        if (hh < part) {  // uniform
             uint32_t mh = extra;
 #pragma unroll
             for (int bb = 0; bb < 3; ++bb)
@@ -246,23 +250,35 @@ __device__ __forceinline__ int gen_best_score_split(uint32_t sl, const uint32_t 
             const uint32_t sh = sl ^ mh;
 #pragma unroll
             for (int l = 0; l < 16; ++l) {
-                // dd = subset size without the last qubit; the upper lane's size is dd + 1
+                // dd = subset size without the top qubits; lane q's size is dd + popc(q)
                 const int dd = __builtin_popcount(hh) + __builtin_popcount(l);
                 uint32_t pc = (uint32_t)__builtin_popcount(sh ^ lo[l]);
-                if (hh == 0 && l == 0) pc = upper ? pc : 64u;  // the empty set (lower lane only)
+                if (hh == 0 && l == 0) pc = q ? pc : 64u;  // the empty set (lane q = 0 only)
                 mn[dd] = min(mn[dd], pc);
             }
         }
     }
-    // partner's minima: upper lanes hold sizes dd + 1 at index dd
-    uint32_t other[kGenW + 1];
+    // lane q holds sizes dd + popc(q) at index dd; lane 0 folds in its partners
+    uint32_t o1[kGenW + 1], o2[kGenW + 1], o3[kGenW + 1];
+    constexpr int w = 64 / S;
 #pragma unroll
-    for (int d = 0; d <= kGenW; ++d) other[d] = (uint32_t)__shfl_xor((int)mn[d], 32);
+    for (int d = 0; d <= kGenW; ++d) o1[d] = (uint32_t)__shfl_xor((int)mn[d], w);  // q ^ 1
+    if constexpr (S == 4) {
+#pragma unroll
+        for (int d = 0; d <= kGenW; ++d) {
+            o2[d] = (uint32_t)__shfl_xor((int)mn[d], 2 * w);      // q ^ 2
+            o3[d] = (uint32_t)__shfl_xor((int)mn[d], 3 * w);      // q ^ 3
+        }
+    }
     int best = INT_MIN;
 #pragma unroll
     for (int d = 1; d <= kGenW; ++d) {
-        const uint32_t m2 = min(mn[d], other[d - 1]);  // lower lane: own size d, partner's size (d-1)+1
-        best = max(best, (base - (int)m2) * (840 / d));
+        uint32_t m = min(mn[d], o1[d - 1]);
+        if constexpr (S == 4) {
+            m = min(m, o2[d - 1]);
+            if (d >= 2) m = min(m, o3[d - 2]);
+        }
+        best = max(best, (base - (int)m) * (840 / d));
     }
     return best;
 }
