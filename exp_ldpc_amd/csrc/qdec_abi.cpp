@@ -463,6 +463,16 @@ void build_tables(qd_graph* G, int m, int n) {
         g.m_pad = (m + 63) / 64 * 64;
         g.n_pad = (n + 63) / 64 * 64;
         g.shape_drc = 0;
+        // LDS-resident min-sum kernel (bp_ms_lds_kernel): edge k of column j (CSC
+        // order) lives at LDS element row * kMlDRS + position in the CSR row
+        g.ml_etab = nullptr;
+        if (g.max_rdeg <= kMlDRS && g.max_cdeg <= kMlDC && ((size_t)m + 1) * kMlDRS < 0xffff) {
+            std::vector<uint16_t> et((size_t)kMlDC * n, 0xffff);
+            for (int i = 0; i < m; ++i)
+                for (int e = rp[i]; e < rp[i + 1]; ++e)
+                    et[(size_t)edge_cpos[e] * n + ci[e]] = (uint16_t)(i * kMlDRS + (e - rp[i]));
+            g.ml_etab = G->arena.upload(et);
+        }
         return;
     }
     g.m_pad = rc * 64;
@@ -521,7 +531,9 @@ void build_tables(qd_graph* G, int m, int n) {
 
 // Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.
 void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
-    if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision, a.B, G->num_cus))) return;
+    if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision, a.B, G->num_cus) &&
+                     !lds_kernel_applies(G->dg, method, precision, a)))
+        return;
     const DevGraph& g = G->dg;
     if (a.B > G->q_cap) {
         ws_drain(G);  // launches still in flight may use the old queue

@@ -686,6 +686,244 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
     }
 }
 
+// ---------------------------------------------------------------- LDS-resident min-sum BP
+// Min-sum BP (fp32) for graphs whose messages spill the small-graph LDS budget
+// but whose v2c rows alone fit one CU's 160 KB LDS (config 4: m = 4800 rows of
+// kMlDRS = 8 floats = 150 KB).  One 1024-thread workgroup per CU decodes one
+// shot at a time with every message on chip:
+//   rows   [m][kMlDRS] f32: v2c messages at (row, CSR position); after the check
+//          pass, slots 0..2 of a row hold the check's state instead: m1 and m2
+//          (minimum and second minimum of |v|, counted with multiplicity) carrying
+//          the row parity in their sign bits, and the position of the minimum
+//   pbuf   two bit arrays of m bits: parity of the hard decision per check,
+//          built by the variable pass with LDS xor atomics (only ones touch it)
+// Thread t owns checks t + 1024 c and variables t + 1024 r.  A variable keeps
+// in registers only its messages' old signs (one bit per edge): with the
+// argmin position in the state, c_k = alpha * ((k's position == argmin) ? m2 :
+// m1) picks the same value as ldpc's leave-one-out minimum (when the minimum is
+// tied, m2 = m1 and every edge gets m1 either way), and the sign is parity ^
+// (v_k <= 0).  Per iteration (3 barriers):
+//   A  check pass: syndrome test of the previous iteration's hard decision
+//      (parity bits vs syndrome), then the state of iteration it into slots 0..2
+//   B  barrier-or: all checks satisfied -> converged at it - 1
+//   C  variable pass: gather states, c_k, prefix / suffix sums (ldpc's order),
+//      hard decision, parity xors; new v2c kept in registers
+//   D  barrier (every state read before any row slot is overwritten)
+//   E  scatter v2c into the rows, barrier
+// Finished shots go to the SSF queue exactly as from bp_lane_kernel (hard
+// decision, residual, converged bit); ssf_block_kernel runs SSF and finalises.
+// Pad edges (k >= the column's degree, variables j >= n) point at a dummy row m:
+// they gather garbage that the sums mask out, scatter into it and xor parity
+// bit m, so the loops have no per-edge branches.
+constexpr int kMlThreads = 1024;
+
+__host__ __device__ inline size_t ml_pbuf_words(const DevGraph& g) { return ((size_t)g.m + 1 + 31) / 32 + 3 & ~(size_t)3; }
+__host__ __device__ inline size_t ml_lds_bytes(const DevGraph& g) {
+    return kCtrl + ((size_t)g.m + 1) * kMlDRS * 4 + 2 * 4 * ml_pbuf_words(g) + 2 * 4 * (kMlThreads / 64);
+}
+
+template <int VPT>
+__global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, DecodeArgs a,
+                                                              const uint16_t* __restrict__ etab,
+                                                              const float* __restrict__ prior) {
+    static_assert(VPT * kMlDC <= 64, "sign bits");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    long long* next = reinterpret_cast<long long*>(smem + 56);
+    float* rows = reinterpret_cast<float*>(smem + kCtrl);
+    const int tid = threadIdx.x;
+    const int m = g.m, n = g.n;
+    const int npw = (m + 1 + 31) / 32;
+    const uint32_t pbw = (uint32_t)ml_pbuf_words(g);
+    uint32_t* pb0 = reinterpret_cast<uint32_t*>(rows + ((size_t)m + 1) * kMlDRS);
+    int* flags = reinterpret_cast<int*>(pb0 + 2 * pbw);  // [2][16]
+    const uint32_t pad = (uint32_t)m * kMlDRS;
+    const int ncr = (m - tid + kMlThreads - 1) / kMlThreads;  // checks of this thread (<= 32)
+    if (blockIdx.x == 0 && tid == 0) *a.q_count = (int32_t)a.B;
+
+    // per-variable constants: prior, degree, LDS element of each edge (u16 pairs)
+    float L[VPT];
+    uint32_t ep[VPT][kMlDC / 2];
+    uint64_t cdeg = 0;  // 3 bits per owned variable (VPT <= 16: 48 bits)
+#pragma unroll
+    for (int r = 0; r < VPT; ++r) {
+        const int j = r * kMlThreads + tid;
+        L[r] = j < n ? prior[j] : 0.0f;
+        int d = 0;
+#pragma unroll
+        for (int h = 0; h < kMlDC / 2; ++h) {
+            uint32_t e0 = pad, e1 = pad;
+            if (j < n) {
+                e0 = etab[(size_t)(2 * h) * n + j];
+                e1 = etab[(size_t)(2 * h + 1) * n + j];
+                d += (e0 != 0xffffu) + (e1 != 0xffffu);
+                e0 = e0 == 0xffffu ? pad : e0;
+                e1 = e1 == 0xffffu ? pad : e1;
+            }
+            ep[r][h] = e0 | (e1 << 16);
+        }
+        cdeg |= (uint64_t)d << (3 * r);
+    }
+    auto edge = [&](int r, int k) -> uint32_t { return (ep[r][k >> 1] >> (16 * (k & 1))) & 0xffffu; };
+    // Keeps the compiler from hoisting the per-edge addresses, positions and
+    // parity masks derived from ep out of the iteration loop (5 live values per
+    // edge instead of half a register): they are re-derived where used.
+    auto opaque_edges = [&]() {
+#pragma unroll
+        for (int r = 0; r < VPT; ++r)
+#pragma unroll
+            for (int h = 0; h < kMlDC / 2; ++h) asm volatile("" : "+v"(ep[r][h]));
+        asm volatile("" : "+v"(cdeg));
+    };
+    uint32_t rdeg = 0;  // 4 bits per owned check (degrees <= 8), checks c < 8
+    for (int c = 0; c < ncr && c < 8; ++c) {
+        const int i = c * kMlThreads + tid;
+        rdeg |= (uint32_t)(g.row_ptr[i + 1] - g.row_ptr[i]) << (4 * c);
+    }
+
+    for (;;) {
+        if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
+        __syncthreads();
+        const int64_t shot = *next;
+        if (shot >= a.B) break;
+        uint32_t sb = 0;  // syndrome bits of the owned checks
+        for (int c = 0; c < ncr; ++c) sb |= (uint32_t)(a.syn[shot * m + c * kMlThreads + tid] & 1) << c;
+        // v2c = prior on every edge; old signs
+        uint64_t sg = 0;  // bit r * kMlDC + k: v2c message k of variable r is <= 0
+        opaque_edges();
+#pragma unroll
+        for (int r = 0; r < VPT; ++r)
+#pragma unroll
+            for (int k = 0; k < kMlDC; ++k) {
+                rows[edge(r, k)] = L[r];
+                sg |= (uint64_t)(L[r] <= 0.0f) << (r * kMlDC + k);
+            }
+        __syncthreads();
+
+        uint32_t xb = 0, bad = 0;  // hard decisions (bit r), failing owned checks (bit c)
+        bool conv = false;
+        int it = 1;
+        for (;; ++it) {
+            // ---- A: test of iteration it - 1, then the check state of iteration it
+            const uint32_t* pprev = pb0 + ((it - 1) & 1) * pbw;
+            uint32_t* pcur = pb0 + (it & 1) * pbw;
+            const bool work = it <= a.max_iter;
+            bad = 0;
+            for (int c = 0; c < ncr; ++c) {
+                const int i = c * kMlThreads + tid;
+                if (it > 1) bad |= (((pprev[i >> 5] >> (i & 31)) ^ (sb >> c)) & 1u) << c;
+                if (work) {
+                    const int deg = c < 8 ? (int)((rdeg >> (4 * c)) & 15u) : (g.row_ptr[i + 1] - g.row_ptr[i]);
+                    float v[kMlDRS];
+                    lds_load<float, kMlDRS>(rows + (size_t)i * kMlDRS, v);
+                    float m1 = Big<float>::v, m2 = Big<float>::v;
+                    int amin = 0;
+                    uint32_t par = (sb >> c) & 1u;
+#pragma unroll
+                    for (int t = 0; t < kMlDRS; ++t) {
+                        const float vt = t < deg ? v[t] : Big<float>::v;
+                        const float av = fabsf(vt);
+                        amin = av < m1 ? t : amin;
+                        m2 = med3(av, m1, m2);
+                        m1 = med3(av, m1, -Big<float>::v);
+                        par ^= vt <= 0.0f;
+                    }
+                    float4 st;
+                    st.x = par ? -m1 : m1;
+                    st.y = par ? -m2 : m2;
+                    st.z = __int_as_float(amin);
+                    st.w = 0.0f;
+                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS) = st;
+                }
+            }
+            if (work)
+                for (int w = tid; w < npw; w += kMlThreads) pcur[w] = 0u;
+            // block-wide "any check failing": one flag per wave, double-buffered by
+            // iteration parity so one barrier suffices
+            int* fl = flags + (it & 1) * (kMlThreads / 64);
+            const unsigned long long wb = __ballot(bad != 0u);
+            if ((tid & 63) == 0) fl[tid >> 6] = wb != 0ull;
+            __syncthreads();
+            int any_bad = 0;
+#pragma unroll
+            for (int w = 0; w < kMlThreads / 64; ++w) any_bad |= fl[w];
+            if (it > 1 && !any_bad) {
+                conv = true;
+                break;
+            }
+            if (!work) break;
+            // ---- C: variable pass (new messages stay in registers until E)
+            const float alpha = alpha_at<float>(it, a.ms_scaling);
+            opaque_edges();
+            float out[VPT][kMlDC];
+            xb = 0;
+#pragma unroll
+            for (int r = 0; r < VPT; ++r) {
+                const int dj = (int)((cdeg >> (3 * r)) & 7u);
+                float c[kMlDC];
+#pragma unroll
+                for (int k = 0; k < kMlDC; ++k) {
+                    const uint32_t e = edge(r, k);
+                    const float4 st = *reinterpret_cast<const float4*>(rows + (e & ~(uint32_t)(kMlDRS - 1)));
+                    const float y = ((int)(e & (kMlDRS - 1)) == __float_as_int(st.z)) ? st.y : st.x;
+                    const float yk = y * alpha;
+                    c[k] = ((sg >> (r * kMlDC + k)) & 1) ? -yk : yk;
+                }
+                // ldpc's order: prefix sums from the prior, then each outgoing
+                // message = prefix + (sum of the later edges, accumulated from the end)
+                float pre[kMlDC];
+                float acc = L[r];
+#pragma unroll
+                for (int k = 0; k < kMlDC; ++k) {
+                    pre[k] = acc;
+                    acc = k < dj ? acc + c[k] : acc;
+                }
+                const bool x = acc <= 0.0f;
+                xb |= (uint32_t)x << r;
+                float suf = 0.0f;
+                bool started = false;
+#pragma unroll
+                for (int k = kMlDC - 1; k >= 0; --k) {
+                    const float o = started ? pre[k] + suf : pre[k];
+                    suf = started ? suf + c[k] : c[k];
+                    started = started || k < dj;
+                    out[r][k] = o;
+                    const uint64_t bit = 1ull << (r * kMlDC + k);
+                    sg = (o <= 0.0f) ? (sg | bit) : (sg & ~bit);
+                }
+                if (x) {
+#pragma unroll
+                    for (int k = 0; k < kMlDC; ++k) {
+                        const uint32_t i = edge(r, k) / kMlDRS;
+                        atomicXor(&pcur[i >> 5], 1u << (i & 31));
+                    }
+                }
+                // one variable's gathers in flight at a time (otherwise the
+                // scheduler hoists all of them and spills)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+            // ---- E: scatter
+            opaque_edges();
+#pragma unroll
+            for (int r = 0; r < VPT; ++r)
+#pragma unroll
+                for (int k = 0; k < kMlDC; ++k) rows[edge(r, k)] = out[r][k];
+            __syncthreads();
+        }
+        // ---- queue the shot: hard decision, residual syndrome, converged bit
+#pragma unroll
+        for (int r = 0; r < VPT; ++r) {
+            const int j = r * kMlThreads + tid;
+            if (j < n) a.q_x[shot * n + j] = (uint8_t)((xb >> r) & 1);
+        }
+        for (int c = 0; c < ncr; ++c) a.q_r[shot * m + c * kMlThreads + tid] = (uint8_t)((bad >> c) & 1);
+        if (tid == 0) {
+            a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
+            if (a.iters) a.iters[shot] = conv ? it - 1 : a.max_iter;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launcher
 template <typename K, typename P>
 static int launch_block(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, int cap_per_cu,
@@ -781,6 +1019,58 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
     rc = launch_block2(ssf_block_kernel, small, a.B, num_cus, stream, g, a);
     record_ev(a, 2, stream);
     return rc;
+}
+
+// ---------------------------------------------------------------- LDS-resident launch
+// QDEC_LDS_KERNEL=0 disables bp_ms_lds_kernel, =1 forces it on any graph it can
+// hold (also those whose messages fit the small-graph LDS budget); by default
+// it takes the min-sum fp32 graphs whose messages would go to HBM.
+bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a) {
+    if (method != 1 || precision != 1 || !g.ml_etab) return false;
+    if (!a.syn || a.syn_flags || a.llr_out || !a.wave_ctr) return false;
+    if (g.n > 16 * kMlThreads || g.m <= 0 || ml_lds_bytes(g) > 160 * 1024) return false;
+    if (block_placement(g, 4) == 0) return false;  // the SSF/finalize state would not fit LDS
+    const char* opt = getenv("QDEC_LDS_KERNEL");
+    if (opt && opt[0] == '0') return false;
+    if (opt && opt[0] == '1') return true;
+    return block_placement(g, 4) != 3;
+}
+
+template <int VPT>
+static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    const size_t lds = ml_lds_bytes(g);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bp_ms_lds_kernel<VPT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_ms_lds_kernel<VPT>, kMlThreads, lds);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    const long long grid = std::min<long long>((long long)num_cus * per_cu, a.B);
+    e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);  // shot counter
+    if (e != hipSuccess) return (int)e;
+    record_ev(a, 0, stream);
+    hipLaunchKernelGGL((bp_ms_lds_kernel<VPT>), dim3((unsigned)grid), dim3(kMlThreads), lds, stream, g, a, g.ml_etab,
+                       reinterpret_cast<const float*>(g.prior[1][1]));
+    const hipError_t le = hipGetLastError();
+    record_ev(a, 1, stream);
+    if (le != hipSuccess) return (int)le;
+    const bool fin_hbm = block_placement(g, 4) == 0;
+    const int rc = fin_hbm ? (int)hipErrorNotSupported
+                           : launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus, stream, g,
+                                           a);
+    record_ev(a, 2, stream);
+    return rc;
+}
+
+static int launch_lds(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+    const int vpt = (g.n + kMlThreads - 1) / kMlThreads;
+    if (vpt <= 4) return launch_lds_typed<4>(g, a, num_cus, stream);
+    if (vpt <= 8) return launch_lds_typed<8>(g, a, num_cus, stream);
+    if (vpt <= 10) return launch_lds_typed<10>(g, a, num_cus, stream);
+    if (vpt <= 12) return launch_lds_typed<12>(g, a, num_cus, stream);
+    return launch_lds_typed<16>(g, a, num_cus, stream);
 }
 
 // ---------------------------------------------------------------- shot-lane launch
@@ -889,6 +1179,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
                   : (c4 ? launch_lane_typed<double, 16, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
                         : launch_lane_typed<double, 16, 8>(g, a, num_cus, stream, scratch, scratch_bytes));
     }
+    if (lds_kernel_applies(g, method, precision, a)) return launch_lds(g, a, num_cus, stream);
     if (precision == 1)
         return method == 1 ? launch_block_typed<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_block_typed<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);

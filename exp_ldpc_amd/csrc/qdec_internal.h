@@ -9,6 +9,8 @@ namespace qdec {
 constexpr int kWave = 64;        // CDNA wavefront
 constexpr int kDR = 8;           // max check degree of the wave kernels
 constexpr int kDC = 4;           // max variable degree of the wave kernels
+constexpr int kMlDRS = 8;        // LDS-resident min-sum kernel: row stride (elements), max check degree
+constexpr int kMlDC = 4;         // LDS-resident min-sum kernel: max variable degree
 constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
 constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
 constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
@@ -75,6 +77,10 @@ struct DevGraph {
     const uint16_t* ms_vslot;     // [n_pad] column held by lane slot s (pads: n_pad + s % 64)
     const void* ms_prior[2];      // [precision][n_pad] min-sum priors in slot order
     int ms_d3r;                   // leading 64-slot rounds whose variables all have degree <= 3
+    // LDS-resident min-sum workgroup kernel (qdec_bp_block.hip, bp_ms_lds_kernel):
+    // [kMlDC][n] LDS element of edge k of column j (row * kMlDRS + CSR position),
+    // pad 0xffff; nullptr when the graph's degrees exceed kMlDRS / kMlDC
+    const uint16_t* ml_etab;
     // flip sets (SSF)
     int n_gen, g_pad, g_wmax;
     const uint8_t* g_w;           // [g_pad]
@@ -169,6 +175,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
 int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream);
 size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, int64_t B);
 bool lane_kernel_applies(const DevGraph& g, int method, int precision, int64_t B, int num_cus);
+bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a);
 size_t lane_slot_bytes(const DevGraph& g, size_t tsz);
 int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,
                           uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,

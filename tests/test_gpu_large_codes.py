@@ -159,3 +159,49 @@ def test_psl13_spacetime_r1_product_sum_f32(gpu_available, oracle_lib, psl13_hz)
     syn, rd = oracle_lib.sample_storage(hz, 1, p, p, seed=SEED, stream=9, shot0=0, B=12)
     _decode_both(oracle_lib, H, 2 * p / 3, syn, max_iter=8, method="ps", precision="f32",
                  keys=("x", "corr", "iters", "status"), n_data=hz.shape[1], fold_blocks=2)
+
+
+@pytest.mark.parametrize("p", [0.01, 0.03, 0.06])
+def test_hgp10k_lds_kernel_parity(gpu_available, oracle_lib, hgp10k, p):
+    """C4 on the LDS-resident min-sum kernel (bp_ms_lds_kernel, the default for
+    fp32 min-sum on this graph): hard decisions, iteration counts, SSF steps,
+    corrections and failure flags bit-exact at low, medium and high p (the last
+    one runs most shots to max_iter)."""
+    hx, hz, lz = hgp10k
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=11, shot0=0, B=256)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=50, keys=KEYS_SSF)
+    if p >= 0.03:
+        assert (got["status"] & 1).mean() < 0.9 and got["ssf_steps"].sum() > 0
+
+
+def test_hgp10k_workgroup_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
+    """The HBM-message workgroup kernel stays covered on C4 (QDEC_LDS_KERNEL=0)."""
+    monkeypatch.setenv("QDEC_LDS_KERNEL", "0")
+    hx, hz, lz = hgp10k
+    p = 0.03
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=12, shot0=0, B=96)
+    _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=30, keys=KEYS_SSF)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatch):
+    """bp_ms_lds_kernel forced (QDEC_LDS_KERNEL=1) on ragged graphs outside the wave
+    shapes: check degrees 0..8 (empty and single-edge rows), variable degrees
+    0..4, per-column priors, ms_scaling both ways; x / iterations / status."""
+    from exp_ldpc_amd.codes import make_check_matrix
+    monkeypatch.setenv("QDEC_LDS_KERNEL", "1")
+    rng = np.random.default_rng(seed)
+    m, n = int(rng.integers(600, 1500)), int(rng.integers(700, 3000))
+    rows, colcount = [], np.zeros(n, int)
+    for i in range(m):
+        d = int(rng.integers(0, 9))
+        cand = [j for j in rng.permutation(n) if colcount[j] < 4][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    H = make_check_matrix(rows, n)
+    e = (rng.random((300, n)) < 0.02).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.uniform(0.005, 0.1, n)
+    for scaling in (0.0, 0.625):
+        _decode_both(oracle_lib, H, probs, syn, max_iter=30, ms_scaling=scaling)

@@ -108,6 +108,7 @@ def run(name, shots, ps_override, reps, batch=None):
             "bp_kernel_ms_per_launch": float(bp_ms.mean()), "ssf_kernel_ms_per_launch": float(ssf_ms.mean()),
             "E": E, "algorithmic_GBps_bp_kernel": bytes_per_pass / kernel_s / 1e9,
             "lane_kernel": os.environ.get("QDEC_LANE_KERNEL", "0") == "1",
+            "lds_kernel_env": os.environ.get("QDEC_LDS_KERNEL", "default"),
         }
         print(json.dumps(res), flush=True)
         del syn, rd
