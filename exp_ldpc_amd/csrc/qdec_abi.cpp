@@ -466,7 +466,7 @@ void build_tables(qd_graph* G, int m, int n) {
         // LDS-resident min-sum kernel (bp_ms_lds_kernel): edge k of column j (CSC
         // order) lives at LDS element row * kMlDRS + position in the CSR row
         g.ml_etab = nullptr;
-        if (g.max_rdeg <= kMlDRS && g.max_cdeg <= kMlDC && ((size_t)m + 1) * kMlDRS < 0xffff) {
+        if (g.max_rdeg <= kMlDRS && g.max_cdeg <= kMlDC && (size_t)m * kMlDRS + 64 < 0xffff) {
             std::vector<uint16_t> et((size_t)kMlDC * n, 0xffff);
             for (int i = 0; i < m; ++i)
                 for (int e = rp[i]; e < rp[i + 1]; ++e)
@@ -723,6 +723,7 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
             for (int c = 0; c < kGenLC; ++c) lc8[(size_t)(c / 4) * gp + gi] |= (uint32_t)g.m_pad << (8 * (c % 4));
         int wmax = 0, nlcmax = 0;
         std::vector<std::vector<uint16_t>> inv(g.m_pad);  // check -> (generator, local bit)
+        std::vector<std::vector<uint32_t>> inv_all(g.m);  // the same for every generator (block SSF)
         for (int gi = 0; gi < n_gen; ++gi) {
             const int a = gen_ptr[gi], b = gen_ptr[gi + 1];
             if (b < a) throw Fail(-31, "gen_ptr not monotone");
@@ -745,6 +746,7 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
             for (size_t c = 0; c < checks.size(); ++c) {
                 lc[c * gp + gi] = (uint16_t)checks[c];
                 if (gi < 256) inv[checks[c]].push_back((uint16_t)(gi | (c << 8)));
+                inv_all[checks[c]].push_back((uint32_t)gi | ((uint32_t)c << 16));
                 uint32_t& word = lc8[(c / 4) * gp + gi];
                 word = (word & ~(0xffu << (8 * (c % 4)))) | ((uint32_t)checks[c] << (8 * (c % 4)));
             }
@@ -786,6 +788,18 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         g.g_qmask = G->flip_arena.upload(qm);
         if (pack8) g.g_lc8 = G->flip_arena.upload(lc8);
         g.g_nlcmax = nlcmax;
+        g.g_iptr = nullptr;
+        g.g_ient = nullptr;
+        if (n_gen < 65536) {
+            std::vector<int32_t> iptr(g.m + 1, 0);
+            std::vector<uint32_t> ient;
+            for (int i = 0; i < g.m; ++i) {
+                ient.insert(ient.end(), inv_all[i].begin(), inv_all[i].end());
+                iptr[i + 1] = (int32_t)ient.size();
+            }
+            g.g_iptr = G->flip_arena.upload(iptr);
+            g.g_ient = G->flip_arena.upload(ient);
+        }
         g.n_gen = n_gen;
         g.g_pad = gp;
         g.g_wmax = wmax;

@@ -473,6 +473,142 @@ __global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArg
     }
 }
 
+// Incremental small-set-flip for queued shots (same spec and keys as
+// ssf_block_kernel, one workgroup per shot): every generator's local syndrome
+// and best key are cached in LDS, and a step only re-scores the generators
+// whose local syndrome it changed (found through the check -> generator inverse
+// table g_iptr / g_ient), instead of re-gathering and re-scoring all of them.
+// Key (int32): score << 13 | (8191 - g), so a signed max picks the highest
+// score, then the lowest g; the lowest subset reaching that score is found
+// afterwards by wave 0 (as in ssf_wave_kernel).
+//   LDS: ctrl | key[g_pad] i32 | slg[g_pad] u32 | dlist[g_pad] u16 | dbits
+//        [g_pad/32] | xh[n_pad] | sres[m_pad] | lpar[k]
+__host__ __device__ inline size_t ssf_inc_lds(const DevGraph& g) {
+    const size_t gp = (size_t)g.g_pad;
+    return kCtrl + gp * 4 + gp * 4 + (gp * 2 + 15) / 16 * 16 + ((gp + 31) / 32 * 4 + 15) / 16 * 16 +
+           ((size_t)g.n_pad + 15) / 16 * 16 + ((size_t)g.m_pad + 15) / 16 * 16 + 4 * (size_t)(g.k > 0 ? g.k : 1);
+}
+
+__global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    long long* redl = reinterpret_cast<long long*>(smem);
+    int* redi = reinterpret_cast<int*>(smem + 32);
+    int* ctl = reinterpret_cast<int*>(smem + 48);  // [0] dirty count, [1] chosen subset
+    const size_t gp = (size_t)g.g_pad;
+    int* key = reinterpret_cast<int*>(smem + kCtrl);
+    uint32_t* slg = reinterpret_cast<uint32_t*>(key + gp);
+    uint16_t* dlist = reinterpret_cast<uint16_t*>(slg + gp);
+    uint32_t* dbits = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(dlist) + (gp * 2 + 15) / 16 * 16);
+    uint8_t* xh = reinterpret_cast<uint8_t*>(dbits) + ((gp + 31) / 32 * 4 + 15) / 16 * 16;
+    uint8_t* sres = xh + ((size_t)g.n_pad + 15) / 16 * 16;
+    int* lpar = reinterpret_cast<int*>(sres + ((size_t)g.m_pad + 15) / 16 * 16);
+    const int tid = threadIdx.x, m = g.m, n = g.n, ng = g.n_gen;
+    const int count = *a.q_count;
+    const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
+    for (int w = tid; w < (int)((gp + 31) / 32); w += kBlock) dbits[w] = 0u;
+    if (tid == 0) ctl[0] = 0;
+    auto rescore = [&](int gi) {
+        const uint32_t sl = slg[gi];
+        if (sl == 0u) {
+            key[gi] = INT_MIN;
+            return;
+        }
+        uint32_t qm[kGenW];
+#pragma unroll
+        for (int k = 0; k < kGenW; ++k) qm[k] = g.g_qmask[k * gp + gi];
+        key[gi] = (int)((unsigned)gen_best_score(sl, qm, nhi) << 13) | (8191 - gi);
+    };
+    for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+        const int64_t qv = a.q_idx[slot];
+        const int64_t shot = qv & ((1ll << 62) - 1);
+        const bool bp_conv = (qv >> 62) & 1;
+        for (int j = tid; j < n; j += kBlock) xh[j] = a.q_x[(int64_t)slot * n + j];
+        int wl = 0;
+        for (int i = tid; i < m; i += kBlock) {
+            const uint8_t r = a.q_r[(int64_t)slot * m + i];
+            sres[i] = r;
+            wl += r;
+        }
+        int sw = block_sum_i32(wl, redi);  // includes a barrier: LDS fills visible
+        int steps = 0;
+        if (a.ssf && sw > 0) {
+            for (int gi = tid; gi < ng; gi += kBlock) {
+                const int nlc = g.g_nlc[gi];
+                uint32_t sl = 0;
+                for (int c = 0; c < nlc; ++c) sl |= (uint32_t)sres[g.g_lc[c * gp + gi]] << c;
+                slg[gi] = sl;
+                rescore(gi);
+            }
+            __syncthreads();
+            while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
+                long long best = LLONG_MIN;
+                for (int gi = tid; gi < ng; gi += kBlock) best = max(best, (long long)key[gi]);
+                best = block_max_i64(best, redl);
+                const int kv = (int)best;
+                const int score = kv >> 13;
+                if (best == LLONG_MIN || kv == INT_MIN || score <= 0) break;
+                const int gsel = 8191 - (kv & 8191);
+                const int w = g.g_w[gsel];
+                if (tid < 64) {  // wave 0: the lowest subset reaching the score
+                    const uint32_t sl = slg[gsel];
+                    const int base = __builtin_popcount(sl);
+                    uint32_t qs[kGenW];
+#pragma unroll
+                    for (int k = 0; k < kGenW; ++k) qs[k] = g.g_qmask[k * gp + gsel];
+                    int tsel = -1;
+                    for (int t0 = 0; t0 < 16 * nhi; t0 += 64) {
+                        const int t = t0 + tid;
+                        uint32_t mt = 0;
+#pragma unroll
+                        for (int k = 0; k < kGenW; ++k) mt ^= ((t >> k) & 1) ? qs[k] : 0u;
+                        const int gain = base - __builtin_popcount(sl ^ mt);
+                        const bool hit = t > 0 && t < 16 * nhi && gain * kSsfScale == score * __builtin_popcount(t);
+                        const unsigned long long hb = __ballot(hit);
+                        if (hb) {
+                            tsel = t0 + __builtin_ctzll(hb);
+                            break;
+                        }
+                    }
+                    if (tid == 0) ctl[1] = tsel;
+                }
+                __syncthreads();
+                const int tsel = ctl[1];
+                if (tsel <= 0) break;  // unreachable: the best score is some subset's score
+                const int gain = score * __builtin_popcount(tsel) / kSsfScale;
+                uint32_t mask = 0;
+                for (int k = 0; k < w; ++k)
+                    if ((tsel >> k) & 1) mask ^= g.g_qmask[k * gp + gsel];
+                // flip: residual, hard decision, and every generator's local syndrome
+                // bit of each flipped check (those generators are queued for re-scoring)
+                if (tid < g.g_nlc[gsel] && ((mask >> tid) & 1)) {
+                    const int c = g.g_lc[tid * gp + gsel];
+                    sres[c] ^= 1;
+                    for (int e = g.g_iptr[c]; e < g.g_iptr[c + 1]; ++e) {
+                        const uint32_t ent = g.g_ient[e];
+                        const int g2 = (int)(ent & 0xffffu);
+                        atomicXor(&slg[g2], 1u << (ent >> 16));
+                        const uint32_t bit = 1u << (g2 & 31);
+                        if (!(atomicOr(&dbits[g2 >> 5], bit) & bit)) dlist[atomicAdd(&ctl[0], 1)] = (uint16_t)g2;
+                    }
+                }
+                if (tid < w && ((tsel >> tid) & 1)) xh[g.g_q[tid * gp + gsel]] ^= 1;
+                __syncthreads();
+                const int nd = ctl[0];
+                for (int d = tid; d < nd; d += kBlock) {
+                    const int g2 = dlist[d];
+                    dbits[g2 >> 5] = 0u;  // whole word: every generator in it is being re-scored or clean
+                    rescore(g2);
+                }
+                __syncthreads();
+                if (tid == 0) ctl[0] = 0;
+                sw -= gain;
+                ++steps;
+            }
+        }
+        finalize_block(g, a, shot, xh, bp_conv, sw == 0, steps, lpar);
+    }
+}
+
 // ---------------------------------------------------------------- shot-lane BP
 // Min-sum BP for graphs whose messages do not fit LDS (configs 4 and 5: 10^4 to
 // 1.2*10^5 columns), laid out for coalesced HBM streaming.  Lane l of every wave
@@ -712,14 +848,19 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
 //   E  scatter v2c into the rows, barrier
 // Finished shots go to the SSF queue exactly as from bp_lane_kernel (hard
 // decision, residual, converged bit); ssf_block_kernel runs SSF and finalises.
-// Pad edges (k >= the column's degree, variables j >= n) point at a dummy row m:
-// they gather garbage that the sums mask out, scatter into it and xor parity
-// bit m, so the loops have no per-edge branches.
+// Pad edges (k >= the column's degree, variables j >= n) point at dummy rows
+// past row m (element m * kMlDRS + lane, so no two lanes of a wave write the
+// same address): they gather garbage that the sums mask out and scatter into
+// them, so the loops have no per-edge branches; only real edges xor parity.
 constexpr int kMlThreads = 1024;
 
-__host__ __device__ inline size_t ml_pbuf_words(const DevGraph& g) { return ((size_t)g.m + 1 + 31) / 32 + 3 & ~(size_t)3; }
+constexpr int kMlDummyRows = 64 / kMlDRS;  // pad edges of lane l use element m * kMlDRS + l
+
+__host__ __device__ inline size_t ml_pbuf_words(const DevGraph& g) {
+    return ((size_t)g.m + kMlDummyRows + 31) / 32 + 3 & ~(size_t)3;
+}
 __host__ __device__ inline size_t ml_lds_bytes(const DevGraph& g) {
-    return kCtrl + ((size_t)g.m + 1) * kMlDRS * 4 + 2 * 4 * ml_pbuf_words(g) + 2 * 4 * (kMlThreads / 64);
+    return kCtrl + ((size_t)g.m + kMlDummyRows) * kMlDRS * 4 + 2 * 4 * ml_pbuf_words(g) + 2 * 4 * (kMlThreads / 64);
 }
 
 template <int VPT>
@@ -732,36 +873,33 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
     float* rows = reinterpret_cast<float*>(smem + kCtrl);
     const int tid = threadIdx.x;
     const int m = g.m, n = g.n;
-    const int npw = (m + 1 + 31) / 32;
+    const int npw = (m + kMlDummyRows + 31) / 32;
     const uint32_t pbw = (uint32_t)ml_pbuf_words(g);
-    uint32_t* pb0 = reinterpret_cast<uint32_t*>(rows + ((size_t)m + 1) * kMlDRS);
+    uint32_t* pb0 = reinterpret_cast<uint32_t*>(rows + ((size_t)m + kMlDummyRows) * kMlDRS);
     int* flags = reinterpret_cast<int*>(pb0 + 2 * pbw);  // [2][16]
-    const uint32_t pad = (uint32_t)m * kMlDRS;
+    const uint32_t pad0 = (uint32_t)m * kMlDRS;        // first dummy element
+    const uint32_t pad = pad0 + (uint32_t)(tid & 63);  // this lane's (distinct banks, no same-address writes)
     const int ncr = (m - tid + kMlThreads - 1) / kMlThreads;  // checks of this thread (<= 32)
     if (blockIdx.x == 0 && tid == 0) *a.q_count = (int32_t)a.B;
 
     // per-variable constants: prior, degree, LDS element of each edge (u16 pairs)
     float L[VPT];
     uint32_t ep[VPT][kMlDC / 2];
-    uint64_t cdeg = 0;  // 3 bits per owned variable (VPT <= 16: 48 bits)
 #pragma unroll
     for (int r = 0; r < VPT; ++r) {
         const int j = r * kMlThreads + tid;
         L[r] = j < n ? prior[j] : 0.0f;
-        int d = 0;
 #pragma unroll
         for (int h = 0; h < kMlDC / 2; ++h) {
             uint32_t e0 = pad, e1 = pad;
             if (j < n) {
                 e0 = etab[(size_t)(2 * h) * n + j];
                 e1 = etab[(size_t)(2 * h + 1) * n + j];
-                d += (e0 != 0xffffu) + (e1 != 0xffffu);
                 e0 = e0 == 0xffffu ? pad : e0;
                 e1 = e1 == 0xffffu ? pad : e1;
             }
             ep[r][h] = e0 | (e1 << 16);
         }
-        cdeg |= (uint64_t)d << (3 * r);
     }
     auto edge = [&](int r, int k) -> uint32_t { return (ep[r][k >> 1] >> (16 * (k & 1))) & 0xffffu; };
     // Keeps the compiler from hoisting the per-edge addresses, positions and
@@ -772,7 +910,6 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
         for (int r = 0; r < VPT; ++r)
 #pragma unroll
             for (int h = 0; h < kMlDC / 2; ++h) asm volatile("" : "+v"(ep[r][h]));
-        asm volatile("" : "+v"(cdeg));
     };
     uint32_t rdeg = 0;  // 4 bits per owned check (degrees <= 8), checks c < 8
     for (int c = 0; c < ncr && c < 8; ++c) {
@@ -858,7 +995,9 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
             xb = 0;
 #pragma unroll
             for (int r = 0; r < VPT; ++r) {
-                const int dj = (int)((cdeg >> (3 * r)) & 7u);
+                int dj = 0;  // degree: real edges come first, pads point past the rows
+#pragma unroll
+                for (int k = 0; k < kMlDC; ++k) dj += edge(r, k) < pad0;
                 float c[kMlDC];
 #pragma unroll
                 for (int k = 0; k < kMlDC; ++k) {
@@ -894,7 +1033,7 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
 #pragma unroll
                     for (int k = 0; k < kMlDC; ++k) {
                         const uint32_t i = edge(r, k) / kMlDRS;
-                        atomicXor(&pcur[i >> 5], 1u << (i & 31));
+                        if (k < dj) atomicXor(&pcur[i >> 5], 1u << (i & 31));
                     }
                 }
                 // one variable's gathers in flight at a time (otherwise the
@@ -953,6 +1092,27 @@ static int launch_block2(K kern, size_t lds, int64_t work, int num_cus, hipStrea
     if (grid <= 0) return 0;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, stream, g, a, gstate);
     return (int)hipGetLastError();
+}
+
+// SSF + finalize of queued shots whose state fits LDS: the incremental kernel
+// when the inverse table exists (QDEC_SSF_INC=0 selects the re-scanning one).
+static int launch_ssf_fin(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    const char* opt = getenv("QDEC_SSF_INC");
+    const size_t lds = ssf_inc_lds(g);
+    if (a.ssf && g.g_iptr && g.n_gen <= 8192 && lds <= 160 * 1024 && !(opt && opt[0] == '0')) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ssf_inc_block_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+        int per_cu = 0;
+        hipError_t e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ssf_inc_block_kernel, kBlock, lds);
+        if (e2 != hipSuccess) return (int)e2;
+        if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+        const long long grid = std::min<long long>((long long)num_cus * per_cu, a.B);
+        if (grid <= 0) return 0;
+        hipLaunchKernelGGL(ssf_inc_block_kernel, dim3((unsigned)grid), dim3(kBlock), lds, stream, g, a);
+        return (int)hipGetLastError();
+    }
+    return launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus, stream, g, a);
 }
 
 constexpr size_t kLdsMsgLimit = 64 * 1024;  // messages in LDS up to this (2 workgroups per CU)
@@ -1016,7 +1176,7 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
                  : launch_block(bp_block_kernel<T, METHOD, true>, lds, a.B, num_cus, stream, cap, g, a, gs, placement);
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
-    rc = launch_block2(ssf_block_kernel, small, a.B, num_cus, stream, g, a);
+    rc = launch_ssf_fin(g, a, num_cus, stream);
     record_ev(a, 2, stream);
     return rc;
 }
@@ -1057,8 +1217,7 @@ static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus,
     if (le != hipSuccess) return (int)le;
     const bool fin_hbm = block_placement(g, 4) == 0;
     const int rc = fin_hbm ? (int)hipErrorNotSupported
-                           : launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus, stream, g,
-                                           a);
+                           : launch_ssf_fin(g, a, num_cus, stream);
     record_ev(a, 2, stream);
     return rc;
 }
@@ -1103,8 +1262,7 @@ static int launch_lane_typed(const DevGraph& g, const DecodeArgs& a, int num_cus
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;
     const int rc = fin_hbm ? launch_block2(ssf_block_kernel, kCtrl, a.B, num_cus, stream, g, a, fin_state, kFinPerCu)
-                           : launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus,
-                                           stream, g, a);
+                           : launch_ssf_fin(g, a, num_cus, stream);
     record_ev(a, 2, stream);
     return rc;
 }
@@ -1188,7 +1346,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
 }
 
 int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
-    return launch_block2(ssf_block_kernel, (block_small_lds(g) + 15) / 16 * 16, a.B, num_cus, stream, g, a);
+    return launch_ssf_fin(g, a, num_cus, stream);
 }
 
 }  // namespace qdec

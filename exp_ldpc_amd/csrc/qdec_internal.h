@@ -96,6 +96,11 @@ struct DevGraph {
     const uint16_t* g_inv;
     int g_invd, g_invl;
     const uint32_t* g_qmask;      // [kGenW][g_pad]   local-check mask of qubit k
+    // every generator's local checks inverted, CSR by check: entries of check i
+    // are g_ient[g_iptr[i] .. g_iptr[i+1]), each g | (local bit << 16)
+    // (ssf_inc_block_kernel; nullptr when n_gen >= 65536)
+    const int32_t* g_iptr;
+    const uint32_t* g_ient;
     // logicals (fused failure check)
     int k, lz_words;
     const uint64_t* lz;           // [k][lz_words]    bit q%64 of word q/64

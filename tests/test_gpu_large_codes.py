@@ -205,3 +205,14 @@ def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatc
     probs = rng.uniform(0.005, 0.1, n)
     for scaling in (0.0, 0.625):
         _decode_both(oracle_lib, H, probs, syn, max_iter=30, ms_scaling=scaling)
+
+
+def test_hgp10k_ssf_rescan_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
+    """The re-scanning SSF block kernel (QDEC_SSF_INC=0) stays covered; the
+    default incremental one is covered by every other C4 test."""
+    monkeypatch.setenv("QDEC_SSF_INC", "0")
+    hx, hz, lz = hgp10k
+    p = 0.03
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=13, shot0=0, B=96)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=30, keys=KEYS_SSF)
+    assert got["ssf_steps"].sum() > 0
