@@ -418,6 +418,99 @@ tables_done:
     g.ms_smask = G->arena.upload(smask);
 }
 
+// Row positions of the edges for the LDS-resident min-sum kernel
+// (bp_ms_lds_kernel): edge e of row i sits at LDS element i * kMlDRS + pos[e].
+// The check pass is independent of the order inside a row, so positions are
+// free; the variable pass scatters with one ds_write_b32 per (variable round
+// r, wave w, edge k): 2 x 32 lanes, bank = element % 32, cost max(4, L0 + L1)
+// with L_h the worst bank load of half h (pad lanes write element m * kMlDRS +
+// lane).  A seeded hill climb over position swaps inside rows lowers the sum
+// over instructions (tie-break: sum of squared loads).  Cached per graph.
+std::vector<int> ml_positions(int m, int n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
+                              const std::vector<int>& edge_cpos) {
+    struct Entry {
+        std::vector<int32_t> rp, ci;
+        std::vector<int> pos;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const auto& c : cache)
+            if (c.rp == rp && c.ci == ci) return c.pos;
+    }
+    const int E = rp[m];
+    constexpr int NT = 1024, NB = 32;
+    std::vector<int> pos(E), row(E), grp(E), half(E);
+    const int rounds = (n + NT - 1) / NT;
+    const int NG = rounds * (NT / 64) * kMlDC;
+    std::vector<int> load((size_t)NG * 2 * NB, 0);
+    for (int i = 0; i < m; ++i)
+        for (int e = rp[i]; e < rp[i + 1]; ++e) {
+            const int j = ci[e];
+            pos[e] = e - rp[i];
+            row[e] = i;
+            grp[e] = ((j / NT) * (NT / 64) + (j % NT) / 64) * kMlDC + edge_cpos[e];
+            half[e] = (j % 64) / 32;
+        }
+    auto bank = [&](int e) { return (row[e] * kMlDRS + pos[e]) % NB; };
+    for (int e = 0; e < E; ++e) load[((size_t)grp[e] * 2 + half[e]) * NB + bank(e)]++;
+    // pad lanes: variables without a k-th edge, slots past n
+    std::vector<int> cdeg(n, 0);
+    for (int e = 0; e < E; ++e) cdeg[ci[e]]++;
+    for (int s = 0; s < rounds * NT; ++s)
+        for (int k = 0; k < kMlDC; ++k)
+            if (s >= n || k >= cdeg[s]) {
+                const int gi = ((s / NT) * (NT / 64) + (s % NT) / 64) * kMlDC + k;
+                load[((size_t)gi * 2 + (s % 64) / 32) * NB + (m * kMlDRS + s % 64) % NB]++;
+            }
+    auto gcost = [&](int gi) {
+        int sum = 0, sq = 0;
+        for (int h = 0; h < 2; ++h) {
+            int mx = 0;
+            for (int b = 0; b < NB; ++b) {
+                const int v = load[((size_t)gi * 2 + h) * NB + b];
+                mx = std::max(mx, v);
+                sq += v * v;
+            }
+            sum += mx;
+        }
+        return (long)std::max(4, sum) * 100000 + sq;
+    };
+    std::mt19937 rng(2024);
+    std::vector<int> at(kMlDRS);
+    for (long it = 0; it < 40L * E; ++it) {
+        const int i = (int)(rng() % (unsigned)m);
+        const int deg = rp[i + 1] - rp[i];
+        if (deg < 2) continue;
+        const int e1 = rp[i] + (int)(rng() % (unsigned)deg);
+        const int p2 = (int)(rng() % (unsigned)deg);
+        int e2 = -1;
+        for (int e = rp[i]; e < rp[i + 1]; ++e)
+            if (pos[e] == p2) e2 = e;
+        if (e2 == e1 || e2 < 0) continue;
+        const int g1 = grp[e1], g2 = grp[e2];
+        const long before = gcost(g1) + (g2 != g1 ? gcost(g2) : 0);
+        auto move = [&](int e, int np) {
+            load[((size_t)grp[e] * 2 + half[e]) * NB + bank(e)]--;
+            pos[e] = np;
+            load[((size_t)grp[e] * 2 + half[e]) * NB + bank(e)]++;
+        };
+        const int p1 = pos[e1];
+        move(e1, p2);
+        move(e2, p1);
+        const long after = gcost(g1) + (g2 != g1 ? gcost(g2) : 0);
+        if (after > before) {
+            move(e2, p2);
+            move(e1, p1);
+        }
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 8) cache.erase(cache.begin());
+    cache.push_back(Entry{rp, ci, pos});
+    return pos;
+}
+
 void build_tables(qd_graph* G, int m, int n) {
     DevGraph& g = G->dg;
     g.m = m;
@@ -467,10 +560,11 @@ void build_tables(qd_graph* G, int m, int n) {
         // order) lives at LDS element row * kMlDRS + position in the CSR row
         g.ml_etab = nullptr;
         if (g.max_rdeg <= kMlDRS && g.max_cdeg <= kMlDC && (size_t)m * kMlDRS + 64 < 0xffff) {
+            const std::vector<int> pos = ml_positions(m, n, rp, ci, edge_cpos);
             std::vector<uint16_t> et((size_t)kMlDC * n, 0xffff);
             for (int i = 0; i < m; ++i)
                 for (int e = rp[i]; e < rp[i + 1]; ++e)
-                    et[(size_t)edge_cpos[e] * n + ci[e]] = (uint16_t)(i * kMlDRS + (e - rp[i]));
+                    et[(size_t)edge_cpos[e] * n + ci[e]] = (uint16_t)(i * kMlDRS + pos[e]);
             g.ml_etab = G->arena.upload(et);
         }
         return;

@@ -828,7 +828,8 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
 // kMlDRS = 8 floats = 150 KB).  One 1024-thread workgroup per CU decodes one
 // shot at a time with every message on chip:
 //   rows   [m][kMlDRS] f32: v2c messages at (row, CSR position); after the check
-//          pass, slots 0..2 of a row hold the check's state instead: m1 and m2
+//          pass, slots 0..2 or 4..6 (by bit 3 of the row: rows then spread their
+//          state over all 16 four-bank slots) hold the check's state: m1 and m2
 //          (minimum and second minimum of |v|, counted with multiplicity) carrying
 //          the row parity in their sign bits, and the position of the minimum
 //   pbuf   two bit arrays of m bits: parity of the hard decision per check,
@@ -950,14 +951,24 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                 if (it > 1) bad |= (((pprev[i >> 5] >> (i & 31)) ^ (sb >> c)) & 1u) << c;
                 if (work) {
                     const int deg = c < 8 ? (int)((rdeg >> (4 * c)) & 15u) : (g.row_ptr[i + 1] - g.row_ptr[i]);
+                    // state half of the row first (so = 4 * bit 3 of the row: 16
+                    // consecutive rows then start in 16 distinct 4-bank slots);
+                    // loaded element u sits at row position (u + so) & 7
+                    const int so = ((i >> 3) & 1) << 2;
                     float v[kMlDRS];
-                    lds_load<float, kMlDRS>(rows + (size_t)i * kMlDRS, v);
+                    {
+                        const float4 h0 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + so);
+                        const float4 h1 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + (so ^ 4));
+                        v[0] = h0.x, v[1] = h0.y, v[2] = h0.z, v[3] = h0.w;
+                        v[4] = h1.x, v[5] = h1.y, v[6] = h1.z, v[7] = h1.w;
+                    }
                     float m1 = Big<float>::v, m2 = Big<float>::v;
                     int amin = 0;
                     uint32_t par = (sb >> c) & 1u;
 #pragma unroll
-                    for (int t = 0; t < kMlDRS; ++t) {
-                        const float vt = t < deg ? v[t] : Big<float>::v;
+                    for (int u = 0; u < kMlDRS; ++u) {
+                        const int t = (u + so) & (kMlDRS - 1);
+                        const float vt = t < deg ? v[u] : Big<float>::v;
                         const float av = fabsf(vt);
                         amin = av < m1 ? t : amin;
                         m2 = med3(av, m1, m2);
@@ -969,7 +980,7 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                     st.y = par ? -m2 : m2;
                     st.z = __int_as_float(amin);
                     st.w = 0.0f;
-                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS) = st;
+                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + so) = st;
                 }
             }
             if (work)
@@ -1002,7 +1013,8 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
 #pragma unroll
                 for (int k = 0; k < kMlDC; ++k) {
                     const uint32_t e = edge(r, k);
-                    const float4 st = *reinterpret_cast<const float4*>(rows + (e & ~(uint32_t)(kMlDRS - 1)));
+                    // state slots of row e / 8: the half selected by bit 3 of the row (see A)
+                    const float4 st = *reinterpret_cast<const float4*>(rows + ((e & ~(uint32_t)(kMlDRS - 1)) | ((e >> 4) & 4u)));
                     const float y = ((int)(e & (kMlDRS - 1)) == __float_as_int(st.z)) ? st.y : st.x;
                     const float yk = y * alpha;
                     c[k] = ((sg >> (r * kMlDC + k)) & 1) ? -yk : yk;
