@@ -1160,6 +1160,10 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
         // one slice per CU (block_scratch_bytes sizes 4 per CU)
         if (max_wg < num_cus) return (int)hipErrorOutOfMemory;
         cap = (int)(max_wg / num_cus);
+        // QDEC_BLOCK_WG_PER_CU: fewer resident workgroups (diagnostic: a smaller
+        // HBM working set of message slices against more latency hiding)
+        if (const char* wv = getenv("QDEC_BLOCK_WG_PER_CU"))
+            if (atoi(wv) > 0) cap = std::min(cap, atoi(wv));
         a.work_ctr = static_cast<unsigned long long*>(scratch);
         gs = reinterpret_cast<T*>(static_cast<unsigned char*>(scratch) + kLaneHeader);
         const hipError_t e0 = hipMemsetAsync(a.work_ctr, 0, sizeof(unsigned long long), stream);
