@@ -146,6 +146,12 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
     // column pass reads it sequentially and only the row pass's writes scatter
     const int32_t* ecs = g.edge_csc;
     constexpr bool kCsc = DRM > 0;
+    // unrolled min-sum with messages in HBM: v2c in CSC order and c2v in CSR
+    // order instead, so both passes write contiguously and only their reads
+    // scatter.  A scattered 4-byte HBM write costs a partial-sector write-back
+    // (C5: ~30 B of HBM writes per message write, 155 MB per shot); a
+    // scattered read costs a sector fetch without the write-back.
+    const bool vcsc = METHOD == 1 && DRM > 0 && !(placement & 1);
     // placement 0 (byte arrays in HBM): the unrolled instantiation also keeps the
     // hard decision as bits in LDS ([n_pad/64] words, one ballot per wave), so the
     // syndrome test gathers bits from LDS instead of bytes from HBM
@@ -175,7 +181,14 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
             }
             sb[i] = (uint8_t)s;
         }
-        for (int e = tid; e < E; e += kBlock) v2c[e] = prior[ci[e]];  // CSR order: coalesced
+        if (vcsc) {
+            for (int j = tid; j < n; j += kBlock) {
+                const T pj = prior[j];
+                for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[t] = pj;  // CSC order
+            }
+        } else {
+            for (int e = tid; e < E; e += kBlock) v2c[e] = prior[ci[e]];  // CSR order: coalesced
+        }
         __syncthreads();
         int it = 1;
         bool conv = false;
@@ -188,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                     T v[DRM];
 #pragma unroll
                     for (int t = 0; t < DRM; ++t)
-                        if (t < d) v[t] = v2c[e0 + t];
+                        if (t < d) v[t] = v2c[vcsc ? ecs[e0 + t] : e0 + t];
                     T m1 = Big<T>::v, m2 = Big<T>::v;
                     int par = sb[i];
 #pragma unroll
@@ -204,7 +217,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                     for (int t = 0; t < DRM; ++t)
                         if (t < d) {
                             const T y = (fabs(v[t]) == m1) ? m2a : m1a;
-                            c2v[ecs[e0 + t]] = (par ^ (v[t] <= (T)0)) ? -y : y;
+                            c2v[vcsc ? e0 + t : ecs[e0 + t]] = (par ^ (v[t] <= (T)0)) ? -y : y;
                         }
                 } else if constexpr (METHOD == 1) {
                     T m1 = Big<T>::v, m2 = Big<T>::v;
@@ -272,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                         if (t < d) ev[t] = ce[t0 + t];
 #pragma unroll
                     for (int t = 0; t < DCM; ++t)
-                        if (t < d) c[t] = c2v[t0 + t];  // CSC order: contiguous
+                        if (t < d) c[t] = c2v[vcsc ? ev[t] : t0 + t];  // CSC order: contiguous
 #pragma unroll
                     for (int t = 0; t < DCM; ++t)
                         if (t < d) {
@@ -288,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
 #pragma unroll
                     for (int t = DCM - 1; t >= 0; --t)
                         if (t < d) {
-                            v2c[ev[t]] = pre[t] + suf;
+                            v2c[vcsc ? t0 + t : ev[t]] = pre[t] + suf;
                             suf += c[t];
                         }
                 } else if constexpr (METHOD == 1) {
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void bp_block_kernel(DevGraph g, DecodeArgs
                 T acc = prior[j];
                 for (int t = cp[j]; t < cp[j + 1]; ++t) {
                     if constexpr (METHOD == 1) {
-                        acc += c2v[kCsc ? t : ce[t]];
+                        acc += c2v[(kCsc && !vcsc) ? t : ce[t]];
                     } else {
                         acc *= c2v[kCsc ? t : ce[t]];
                         if (isnan(acc)) acc = (T)1;
@@ -1160,10 +1173,15 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
         // one slice per CU (block_scratch_bytes sizes 4 per CU)
         if (max_wg < num_cus) return (int)hipErrorOutOfMemory;
         cap = (int)(max_wg / num_cus);
-        // QDEC_BLOCK_WG_PER_CU: fewer resident workgroups (diagnostic: a smaller
-        // HBM working set of message slices against more latency hiding)
+        // Resident workgroups per CU.  With the shot state in HBM too (placement
+        // 0, the C5 spacetime graph: 3.3 MB of slices per shot) the scattered
+        // message accesses of more resident shots only add HBM traffic: on C5 at
+        // p = 0.005, 4 / 3 / 2 / 1 per CU ran 18.0 / 20.8 / 26.3 / 19.2 k shots/s
+        // (scattered writes), 23.9 / 27.1 / 29.3 k (contiguous writes, vcsc), so
+        // placement 0 runs 2.  QDEC_BLOCK_WG_PER_CU overrides (diagnostic).
+        if (placement == 0) cap = std::min(cap, 2);
         if (const char* wv = getenv("QDEC_BLOCK_WG_PER_CU"))
-            if (atoi(wv) > 0) cap = std::min(cap, atoi(wv));
+            if (atoi(wv) > 0) cap = std::min((int)(max_wg / num_cus), atoi(wv));
         a.work_ctr = static_cast<unsigned long long*>(scratch);
         gs = reinterpret_cast<T*>(static_cast<unsigned char*>(scratch) + kLaneHeader);
         const hipError_t e0 = hipMemsetAsync(a.work_ctr, 0, sizeof(unsigned long long), stream);
