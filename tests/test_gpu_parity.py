@@ -348,3 +348,53 @@ def test_empty_batch_and_buffer_validation(gpu_available):
         dec.decode_device(B, syn=syn[:4])
     with pytest.raises(ValueError):  # host tensor
         dec.decode_device(B, syn=syn.cpu())
+
+
+@pytest.mark.parametrize("name", BLOCK_GRAPHS)
+def test_lds_kernel_block_graphs(gpu_available, oracle_lib, name, monkeypatch):
+    """bp_ms_lds_kernel forced (QDEC_LDS_KERNEL=1) on the workgroup-kernel graphs,
+    min-sum f32 (its only configuration): x / iterations / status bit-exact."""
+    from exp_ldpc_amd.decoder import Decoder
+    monkeypatch.setenv("QDEC_LDS_KERNEL", "1")
+    H, _ = _graph(name)
+    H = sp.csr_matrix(H)
+    rng = np.random.default_rng(len(name) + 1)
+    B = 300
+    e = (rng.random((B, H.shape[1])) < 0.02).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    dec = Decoder(H, 0.015, method="ms", precision="f32", max_iter=25)
+    got = dec.decode(syn, want=("x", "iters", "status"))
+    ref = oracle_lib.decode(H, 0.015, syn, method="ms", precision="f32", max_iter=25)
+    for key in ("x", "iters", "status"):
+        assert np.array_equal(got[key], ref[key]), key
+
+
+def test_lds_kernel_ssf_fold(gpu_available, oracle_lib, code225, monkeypatch):
+    """bp_ms_lds_kernel + the incremental SSF block kernel forced on a block graph
+    with flip sets and logicals, and on the R = 2 spacetime graph with the fold
+    onto the data qubits (fold_blocks = 3) and the fused logical check."""
+    from conftest import load_code
+    from exp_ldpc_amd.decoder import Decoder
+    monkeypatch.setenv("QDEC_LDS_KERNEL", "1")
+    code = load_code("hgp_36_3_4_s42_g4")
+    hx, hz = code.checks.x, code.checks.z
+    rng = np.random.default_rng(9)
+    rd = (rng.random((400, hz.shape[1])) < 0.03).astype(np.uint8)
+    syn = ((hz @ rd.T).T % 2).astype(np.uint8)
+    dec = Decoder(hz, 0.02, method="ms", precision="f32", max_iter=12, flip_sets=hx, logicals=code.logicals.z)
+    keys = ("x", "corr", "iters", "status", "ssf_steps", "fail")
+    got = dec.decode(syn, readout=rd, want=keys)
+    ref = oracle_lib.decode(hz, 0.02, syn, method="ms", precision="f32", max_iter=12, ssf=True, gens=hx,
+                            lz=code.logicals.z, readout=rd, want_llr=False, ssf_impl="fast")
+    for key in keys:
+        assert np.array_equal(got[key], ref[key]), key
+    assert ref["ssf_steps"].sum() > 0
+    H = _spacetime(2)
+    syn, rd = oracle_lib.sample_storage(HZ, 2, 0.01, 0.01, seed=8, stream=1, shot0=0, B=600)
+    lz = code225.logicals.z
+    dec = Decoder(H, 0.0067, method="ms", precision="f32", max_iter=30, n_data=225, fold_blocks=3, logicals=lz)
+    got = dec.decode(syn, readout=rd, want=("corr", "iters", "status", "fail"))
+    ref = oracle_lib.decode(H, 0.0067, syn, method="ms", precision="f32", max_iter=30, n_data=225, fold_blocks=3,
+                            lz=lz, readout=rd, want_llr=False)
+    for key in ("corr", "iters", "status", "fail"):
+        assert np.array_equal(got[key], ref[key]), key
