@@ -149,19 +149,22 @@ __device__ __forceinline__ T alpha_bits(int it, double ms_scaling) {
 // cheap shots or sit on a less loaded SIMD take more of the tail.  The counter
 // result for the following chunk is requested when a chunk is started and read
 // kChunk shots later (its latency hidden by a shot's work).  Every shot < B is
-// produced exactly once; indices >= B end the wave's loop.
+// produced exactly once; indices >= B end the wave's loop.  Without a counter
+// the whole sequence is the static stride (no request is ever issued).
 struct ShotSeq {
-    static constexpr int kChunk = 4;
     int64_t t = 0, rounds0 = 0, base = 0, grid = 1, blk = 0;
-    int left = 0;
+    int left = 0, kChunk = 4;
     unsigned long long pend = 0;  // lane 0: prefetched chunk id
     unsigned long long* ctr = nullptr;
     bool have = false;
-    __device__ ShotSeq(const DecodeArgs& a, int lane) {
-        grid = gridDim.x;
-        blk = blockIdx.x;
-        ctr = a.wave_ctr;
-        rounds0 = ctr ? (a.B * 4 / 5) / grid : (a.B + grid - 1) / grid + 1;
+    __device__ ShotSeq(const DecodeArgs& a, int lane) : ShotSeq(a.B, a.wave_ctr, blockIdx.x, gridDim.x, lane) {}
+    // `total` items over `nw` persistent waves, this one being wave `wid`
+    __device__ ShotSeq(int64_t total, unsigned long long* counter, int64_t wid, int64_t nw, int lane, int chunk = 4) {
+        kChunk = chunk;
+        grid = nw;
+        blk = wid;
+        ctr = counter;
+        rounds0 = ctr ? (total * 4 / 5) / grid : (total + grid - 1) / grid + 1;
         if (ctr && rounds0 == 0) request(lane);
     }
     __device__ void request(int lane) {
@@ -169,7 +172,7 @@ struct ShotSeq {
         have = true;
     }
     __device__ int64_t next(int lane) {
-        if (t < rounds0) {
+        if (t < rounds0 || !ctr) {  // no counter: the static stride throughout
             const int64_t s = blk + t * grid;
             if (++t == rounds0 && ctr) request(lane);
             return s;

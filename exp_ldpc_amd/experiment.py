@@ -315,7 +315,7 @@ class BPDetectorCorrect:
     check matrix of a detector error model (DEM text or dem.DetectorErrorModel);
     ``readout_correction(detector_string)`` returns the corrected observables."""
 
-    def __init__(self, detector_error_model, bp_osd_options: Dict, *, device: int = 0, precision: str = "f32"):
+    def __init__(self, detector_error_model, bp_osd_options: Dict, *, device: int = 0, precision: str = "f64"):
         from .dem import DetectorSpacetimeCode
         self._detector_spacetime_code = DetectorSpacetimeCode(detector_error_model)
         o = bp_osd_options

@@ -221,7 +221,7 @@ def test_bpd_detector_mode_matches_oracle(gpu_available, oracle_lib, rounds):
     ref_fail = ((obs + (ref["x"].astype(np.int64) @ dem.fault_map.toarray().T.astype(np.int64))) % 2).any(1)
     assert np.array_equal(res.fail, ref_fail)
     assert 0 < res.fail.sum() < 3000
-    w = BPDetectorCorrect(storage_experiment_dem(hz, lz, rounds, p, p), opts)
+    w = BPDetectorCorrect(storage_experiment_dem(hz, lz, rounds, p, p), opts, precision="f32")
     for b in range(4):
         corrected = w.readout_correction(np.concatenate([syn_h[b], obs[b]]))
         assert bool(corrected.any()) == bool(ref_fail[b])
