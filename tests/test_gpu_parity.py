@@ -88,6 +88,28 @@ def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, local_syn
     assert ref["ssf_steps"].sum() > 0
 
 
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_bp_ssf_parity_long_queue(gpu_available, oracle_lib, precision, code225):
+    """A queue long enough (2^18 BP failures, >= 16 slots per SSF wave) that the
+    SSF kernel hands out its tail from the slot counter; shots are independent,
+    so a random subset decoded by the oracle checks every output bit-exactly."""
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(18)
+    B = 1 << 18
+    rd = _errors(rng, B, 225, 0.08)
+    syn = ((HZ @ rd.T).T % 2).astype(np.uint8)
+    lz = code225.logicals.z
+    dec = Decoder(HZ, 0.05, method="ms", precision=precision, max_iter=2, flip_sets=HX, logicals=lz)
+    got = dec.decode(syn, readout=rd, want=("x", "corr", "iters", "status", "ssf_steps", "fail"))
+    assert (got["status"] & 1).mean() < 0.05  # nearly every shot went to the SSF queue
+    idx = np.sort(rng.choice(B, 3000, replace=False))  # ~600 of them from counter-handed slots
+    ref = oracle_lib.decode(HZ, 0.05, syn[idx], method="ms", precision=precision, max_iter=2, ssf=True, gens=HX,
+                            lz=lz, readout=rd[idx], want_llr=False)
+    for key in ("x", "corr", "iters", "status", "ssf_steps", "fail"):
+        assert np.array_equal(got[key][idx], ref[key]), key
+    assert ref["ssf_steps"].mean() > 5
+
+
 def test_ssf_bounded_steps(gpu_available, oracle_lib):
     from exp_ldpc_amd.decoder import Decoder
     rng = np.random.default_rng(5)
