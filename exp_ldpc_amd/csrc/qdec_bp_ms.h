@@ -157,7 +157,14 @@ struct ShotSeq {
     unsigned long long pend = 0;  // lane 0: prefetched chunk id
     unsigned long long* ctr = nullptr;
     bool have = false;
-    __device__ ShotSeq(const DecodeArgs& a, int lane) : ShotSeq(a.B, a.wave_ctr, blockIdx.x, gridDim.x, lane) {}
+// BP counter chunk (diagnostic define): 8 / 16 trade fewer atomics at low p
+// (p = 0.001: 0.51 -> 0.45 / 0.47 ms per 2^18 shots) for coarser tail balance
+// at high p (p = 0.1: 7.04 -> 7.08 / 7.50 ms); the sweep's sum is flat at 8
+#ifndef QDEC_BP_CHUNK
+#define QDEC_BP_CHUNK 4
+#endif
+    __device__ ShotSeq(const DecodeArgs& a, int lane)
+        : ShotSeq(a.B, a.wave_ctr, blockIdx.x, gridDim.x, lane, QDEC_BP_CHUNK) {}
     // `total` items over `nw` persistent waves, this one being wave `wid`
     __device__ ShotSeq(int64_t total, unsigned long long* counter, int64_t wid, int64_t nw, int lane, int chunk = 4) {
         kChunk = chunk;
