@@ -117,32 +117,49 @@ def launch_children(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def cpu_baseline(code, ps, args):
-    """Time the CPU oracle (C port of the same algorithm, f64 like ldpc, OpenMP
-    over shots) on a bounded sample of the same workload; its failure counts
-    give the CPU LER curve the GPU curves are compared with."""
-    from oracle import load as load_oracle
-    orc = load_oracle()
+def _cpu_leg(orc, code, ps, per_p, precision, threads):
+    """Decode per_p oracle-sampled shots at every point in `precision`; returns
+    (seconds of decode, failures per point)."""
     hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 64))
-    per_p = args.cpu_shots
     elapsed = 0.0
     fails = {}
     for pi, p in enumerate(ps):
         syn, rd = orc.sample_storage(hz, 0, p, p, seed=SEED, stream=pi, shot0=0, B=per_p, nthreads=threads)
         t0 = time.perf_counter()
-        out = orc.decode(hz, 2 * p / 3, syn, method="ms", precision="f64", max_iter=50, ssf=True, gens=hx, lz=lz,
+        out = orc.decode(hz, 2 * p / 3, syn, method="ms", precision=precision, max_iter=50, ssf=True, gens=hx, lz=lz,
                          readout=rd, want_llr=False, nthreads=threads, ssf_impl="fast")
         elapsed += time.perf_counter() - t0
         fails[f"{p:.6g}"] = int(out["fail"].sum())
+    return elapsed, fails
+
+
+def cpu_baseline(code, ps, args):
+    """Time the CPU oracle (C port of the same algorithm, OpenMP over shots) on a
+    bounded sample of the same workload: f64 like ldpc (the baseline `value`;
+    its failure counts give the CPU LER curve the GPU curves are compared with)
+    and f32 beside it (`variants`, the same-precision figure for the GPU's f32
+    variant line)."""
+    from oracle import load as load_oracle
+    orc = load_oracle()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 64))
+    per_p = args.cpu_shots
+    elapsed, fails = _cpu_leg(orc, code, ps, per_p, "f64", threads)
     total = per_p * len(ps)
-    return {"value": total / elapsed, "unit": "shots/s", "cores": threads, "kind": "port", "dtype": "f64",
-            "sample": f"{per_p} shots at each of the {len(ps)} sweep points (same sampler and seed as the GPU run, "
-                      f"shot indices 0..{per_p - 1}, i.e. the warmup step's shots, disjoint from the timed ones); "
-                      f"BP min-sum f64 max_iter 50 + SSF + logical check, decode only; {elapsed:.1f} s of CPU work "
-                      f"on {threads} threads",
-            "failures_per_point": fails, "shots_per_point": per_p}
+    res = {"value": total / elapsed, "unit": "shots/s", "cores": threads, "kind": "port", "dtype": "f64",
+           "sample": f"{per_p} shots at each of the {len(ps)} sweep points (same sampler and seed as the GPU run, "
+                     f"shot indices 0..{per_p - 1}, i.e. the warmup step's shots, disjoint from the timed ones); "
+                     f"BP min-sum f64 max_iter 50 + SSF + logical check, decode only; {elapsed:.1f} s of CPU work "
+                     f"on {threads} threads",
+           "failures_per_point": fails, "shots_per_point": per_p}
+    per32 = max(1, per_p // 2)
+    if args.variant == "f32" or args.precision == "f32":
+        e32, f32 = _cpu_leg(orc, code, ps, per32, "f32", threads)
+        res["variants"] = [{"dtype": "f32", "value": per32 * len(ps) / e32, "unit": "shots/s", "cores": threads,
+                            "sample": f"{per32} shots per point (shot indices 0..{per32 - 1}), BP min-sum f32, "
+                                      f"otherwise as the f64 leg; {e32:.1f} s of CPU work",
+                            "failures_per_point": f32, "shots_per_point": per32}]
+    return res
 
 
 class FakeDecoder:

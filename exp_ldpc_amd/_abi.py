@@ -58,6 +58,7 @@ SIGNATURES = {
     "qd_graph_destroy": (_i32, [_p]),
     "qd_graph_set_flipsets": (_i32, [_p, _i32, _p, _p]),
     "qd_graph_set_logicals": (_i32, [_p, _i32, _p]),
+    "qd_graph_set_logicals_csr": (_i32, [_p, _i32, _p, _p]),
     "qd_graph_set_priors": (_i32, [_p, _p]),
     "qd_decode_batch": (_i32, [_p, C.POINTER(QdParams), _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "qd_decode_batch_device": (_i32, [_p, C.POINTER(QdParams), _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),

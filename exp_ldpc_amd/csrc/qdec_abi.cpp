@@ -625,8 +625,7 @@ void build_tables(qd_graph* G, int m, int n) {
 
 // Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.
 void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
-    if (a.B <= 0 || (!a.ssf && !lane_kernel_applies(G->dg, method, precision, a.B, G->num_cus) &&
-                     !lds_kernel_applies(G->dg, method, precision, a)))
+    if (a.B <= 0 || (!a.ssf && !lds_kernel_applies(G->dg, method, precision, a)))
         return;
     const DevGraph& g = G->dg;
     if (a.B > G->q_cap) {
@@ -650,8 +649,8 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
     a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
 }
 
-void* message_scratch(qd_graph* G, int method, int precision, int64_t B, size_t* bytes) {
-    const size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus, B);
+void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& a, size_t* bytes) {
+    const size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus, a);
     *bytes = need;
     if (need == 0) return nullptr;
     if (need > G->mws_bytes) {
@@ -766,6 +765,8 @@ int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t*
             G->dg.lz_words = (n_data + 63) / 64;
             G->dg.k = 0;
             G->dg.lz = nullptr;
+            G->dg.lz_ptr = G->dg.lz_idx = nullptr;
+            G->dg.lz_sparse = 0;
             G->dg.n_gen = 0;
             G->dg.g_inv = nullptr;
             G->dg.g_invd = G->dg.g_invl = 0;
@@ -900,6 +901,47 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
     });
 }
 
+// Upload logicals given as CSR supports: the CSR itself (duplicates cancelled,
+// sorted) and, when it stays below 256 MB, the dense bit-packed table the wave
+// kernels and the OSD finalize read.  lz_sparse picks the workgroup finalize's
+// support walk when the supports are small against the dense words.
+static void upload_logicals(qd_graph* G, int32_t k, std::vector<int32_t> ptr, std::vector<int32_t> idx) {
+    DevGraph& g = G->dg;
+    const int W = g.lz_words;
+    G->lz_arena.release();
+    g.lz = nullptr;
+    g.lz_ptr = g.lz_idx = nullptr;
+    g.k = 0;
+    g.lz_sparse = 0;
+    if (k == 0) return;
+    // canonical supports: sorted, pairs cancel
+    std::vector<int32_t> cptr(1, 0), cidx;
+    cidx.reserve(idx.size());
+    for (int r = 0; r < k; ++r) {
+        std::vector<int32_t> row(idx.begin() + ptr[r], idx.begin() + ptr[r + 1]);
+        std::sort(row.begin(), row.end());
+        for (size_t t = 0; t < row.size();) {
+            size_t u = t;
+            while (u < row.size() && row[u] == row[t]) ++u;
+            if ((u - t) & 1) cidx.push_back(row[t]);
+            t = u;
+        }
+        cptr.push_back((int32_t)cidx.size());
+    }
+    if ((size_t)k * W * 8 <= ((size_t)256 << 20)) {
+        std::vector<uint64_t> packed((size_t)k * W, 0);
+        for (int r = 0; r < k; ++r)
+            for (int t = cptr[r]; t < cptr[r + 1]; ++t) packed[(size_t)r * W + cidx[t] / 64] |= 1ull << (cidx[t] % 64);
+        g.lz = G->lz_arena.upload(packed);
+    }
+    g.lz_ptr = G->lz_arena.upload(cptr);
+    g.lz_idx = G->lz_arena.upload(cidx);
+    // a support walk costs ~ one gather per entry, the dense test one word per
+    // (logical, word): walk when that is clearly cheaper, or when there is no table
+    g.lz_sparse = (!g.lz || cidx.size() <= (size_t)k * W / 4) ? 1 : 0;
+    g.k = k;
+}
+
 int qd_graph_set_logicals(qd_graph* G, int32_t k, const uint8_t* lz) {
     return guarded([&] {
         check_graph(G);
@@ -907,14 +949,33 @@ int qd_graph_set_logicals(qd_graph* G, int32_t k, const uint8_t* lz) {
         DevGraph& g = G->dg;
         if (k < 0 || (k > 0 && !lz)) throw Fail(-40, "invalid logicals");
         if (k > 65536) throw Fail(-41, "more than 65536 logicals not supported");
-        const int W = g.lz_words;
-        std::vector<uint64_t> packed((size_t)std::max(k, 1) * W, 0);
-        for (int r = 0; r < k; ++r)
+        std::vector<int32_t> ptr(1, 0), idx;
+        for (int r = 0; r < k; ++r) {
             for (int q = 0; q < g.n_data; ++q)
-                if (lz[(size_t)r * g.n_data + q] & 1) packed[(size_t)r * W + q / 64] |= 1ull << (q % 64);
-        G->lz_arena.release();
-        g.lz = G->lz_arena.upload(packed);
-        g.k = k;
+                if (lz[(size_t)r * g.n_data + q] & 1) idx.push_back(q);
+            ptr.push_back((int32_t)idx.size());
+        }
+        upload_logicals(G, k, std::move(ptr), std::move(idx));
+    });
+}
+
+int qd_graph_set_logicals_csr(qd_graph* G, int32_t k, const int32_t* lz_ptr, const int32_t* lz_idx) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        const DevGraph& g = G->dg;
+        if (k < 0 || (k > 0 && (!lz_ptr || (!lz_idx && lz_ptr[k] > 0)))) throw Fail(-40, "invalid logicals");
+        if (k > 65536) throw Fail(-41, "more than 65536 logicals not supported");
+        std::vector<int32_t> ptr(lz_ptr, lz_ptr + (k > 0 ? k + 1 : 0)), idx;
+        if (k > 0) {
+            if (ptr[0] != 0) throw Fail(-42, "logicals CSR must start at 0");
+            for (int r = 0; r < k; ++r)
+                if (ptr[r + 1] < ptr[r]) throw Fail(-42, "logicals CSR pointers must be non-decreasing");
+            idx.assign(lz_idx, lz_idx + ptr[k]);
+            for (int32_t q : idx)
+                if (q < 0 || q >= g.n_data) throw Fail(-43, "logical support index out of range");
+        }
+        upload_logicals(G, k, std::move(ptr), std::move(idx));
     });
 }
 
@@ -971,7 +1032,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         attach_queue(G, a, p->method, p->precision);
         attach_timing(G, a);
         size_t sb = 0;
-        void* scr = message_scratch(G, p->method, p->precision, B, &sb);
+        void* scr = message_scratch(G, p->method, p->precision, a, &sb);
         const hipStream_t s = (hipStream_t)stream;
         const bool split = G->ssf_stream && G->ssf_stream != s && a.ssf;
         if (split) {
@@ -1035,7 +1096,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         attach_queue(G, a, p->method, p->precision);
         attach_timing(G, a);
         size_t sb = 0;
-        void* scr = message_scratch(G, p->method, p->precision, B, &sb);
+        void* scr = message_scratch(G, p->method, p->precision, a, &sb);
         ws_acquire(G, s);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));

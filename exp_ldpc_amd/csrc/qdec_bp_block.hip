@@ -65,7 +65,26 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
     if (want_fail)
         for (int r = tid; r < g.k; r += kBlock) lpar[r] = 0;
     __syncthreads();
-    if (a.corr_out || want_fail) {
+    const bool walk = want_fail && g.lz_sparse;
+    if (walk) {  // sparse logicals: each thread tests whole logicals on their supports
+        for (int r = tid; r < g.k; r += kBlock) {
+            int par = 0;
+            for (int t = g.lz_ptr[r]; t < g.lz_ptr[r + 1]; ++t) {
+                const int q = g.lz_idx[t];
+                int cb = a.readout[shot * g.n_data + q] ^ (a.base ? a.base[shot * g.n_data + q] : 0);
+                for (int b = 0; b < g.fold_blocks; ++b) cb ^= xh[b * g.n_data + q];
+                par ^= cb & 1;
+            }
+            lpar[r] = par;
+        }
+    }
+    if (a.corr_out && (!want_fail || walk)) {
+        for (int q = tid; q < g.n_data; q += kBlock) {
+            int cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
+            for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+            a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+        }
+    } else if (want_fail && !walk) {
         for (int w0 = tid; w0 < g.lz_words; w0 += kBlock) {
             unsigned long long word = 0;
             for (int b = 0; b < 64; ++b) {
@@ -622,117 +641,153 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
     }
 }
 
-// ---------------------------------------------------------------- shot-lane BP
-// Min-sum BP for graphs whose messages do not fit LDS (configs 4 and 5: 10^4 to
-// 1.2*10^5 columns), laid out for coalesced HBM streaming.  Lane l of every wave
-// of a workgroup works on the shot held by slot l; each workgroup owns a
-// contiguous scratch block of messages stored edge-major, slot-minor
-// (v2c[e][64], c2v[e][64]), so a wave reading edge e of its 64 shots touches one
-// contiguous 256-byte (fp32) run.  v2c is kept in CSR (row) order and c2v in
-// CSC (column) order, so both passes read their input sequentially and only
-// their writes scatter (writes do not stall the wave).
-// Graph indices (row_ptr, col_idx, col_ptr, col_edge, priors) are the same for
-// every lane: scalar loads.  The kLaneWaves waves split the checks (check pass,
-// syndrome test) and the variables (variable pass), with a workgroup barrier
-// between passes.  Slots are refilled as soon as their shot finishes (converged
-// or max_iter): a workgroup-aggregated atomic hands out shot indices, so the
-// work per slot is the shot's own iteration count, not the slowest shot of a
-// group of 64.  Per shot-iteration the HBM traffic is the 16*E-byte message
-// model of SURVEY §8(d) plus n + 2m bytes of hard decisions and syndrome bits.
-// Arithmetic is the block kernel's, operation for operation (row minimum via
-// med3/fmin, column prefix then suffix sums, alpha_t of the shot's own
-// iteration).  Finished shots go to the SSF queue (hard decision, residual,
-// converged bit); ssf_block_kernel runs SSF on the unconverged ones (when
-// asked) and finalises every shot.
-constexpr int kLaneWaves = 8;
-constexpr int kLaneU = 4;     // checks / variables per wave step (loads in flight)
-constexpr int kFinPerCu = 8;  // finalize/SSF workgroups per CU when their state is in HBM
-constexpr size_t kLaneHeader = 256;  // scratch header: the shot counter
+// ---------------------------------------------------------------- slot-group BP
+// BP for graphs whose messages do not fit LDS (configs 4 and 5: 10^4 to 1.3*10^5
+// columns), laid out so every HBM access of the message loops is a whole
+// cache line.  A workgroup of kGrpWaves waves decodes a group of 64 shot slots
+// together: lane l of every wave works on slot l.  The group owns a scratch
+// block in HBM:
+//   v2c [E][64] T   messages by CSR edge, slot-minor: a wave reading edge e of
+//                   its 64 slots reads one contiguous 256-B (fp32) / 512-B run
+//   c2v [E][64] T   by CSC position (the column pass reads it sequentially)
+//   sw  [m]  u64    syndrome bit of check i for every slot (bit l = slot l)
+//   xw  [n]  u64    hard decision of column j for every slot (one ballot)
+//   pw  [m]  u64    parity of check i under the hard decision (residual words)
+//   rw  [n_data] u64  residual readout ^ corr of slots being finalised
+// Per iteration: check pass (waves split the checks, kGrpU checks per step with
+// all their loads issued first), barrier, column pass (waves split the
+// columns), barrier, syndrome test (lanes split the checks: each lane xors the
+// 64-slot hard-decision words of its row, so one pass tests all 64 slots),
+// barrier.  Slots whose shot converged or reached max_iter are finalised
+// (or queued for SSF) and refilled at once from a group-aggregated atomic
+// counter, so a slot's work is its own shot's iteration count.  Refilling
+// writes no messages: a slot's first check pass reads its columns' priors
+// instead of v2c (the same values ldpc initialises the messages to), and its
+// syndrome bits go into sw in one coalesced sweep per refill batch.
+// Outputs of a finished slot come from the words: corr = base ^ xor of the
+// fold blocks' words, fail = any logical's parity over its CSR support of the
+// residual words (64 slots per gather), x as bytes; BP-unconverged shots go
+// to the SSF queue (bytes, as the other BP kernels write it) when SSF is on.
+// Arithmetic is bp_block_kernel's unrolled loops, operation for operation
+// (min-sum: med3/fmin row minimum and ldpc's column prefix/suffix sums;
+// product-sum: ldpc's forward/backward products and NaN guards), with alpha_t
+// of the slot's own iteration.  HBM traffic per shot-iteration: the 16*E-byte
+// message model (fp32; 32*E fp64) plus O(m + n) bytes of words.
+constexpr int kGrpWaves = 8;
+constexpr int kGrpThreads = 64 * kGrpWaves;
+constexpr int kGrpU = 4;              // checks / columns per wave step (loads in flight)
+constexpr int kFinPerCu = 8;          // SSF/finalize workgroups per CU when their state is in HBM
+constexpr size_t kGrpHeader = 256;    // scratch header: the shot counter
 
-template <typename T, int DR, int DC>
-// The graph index arrays come in as separate __restrict__ arguments: with no
-// possible aliasing store the compiler can keep their (wave-uniform) loads on the
-// scalar unit (s_load) instead of issuing one vector load per lane.
-__global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, DecodeArgs a, unsigned char* scratch,
-                                                                  size_t group_bytes,
-                                                                  const int32_t* __restrict__ rp,
-                                                                  const int32_t* __restrict__ ci,
-                                                                  const int32_t* __restrict__ cp,
-                                                                  const int32_t* __restrict__ ce,
-                                                                  const int32_t* __restrict__ ecs,
-                                                                  const T* __restrict__ prior) {
-    __shared__ unsigned long long bad_w[kLaneWaves];
-    __shared__ long long next_base;
-    // wave index as a scalar: every graph index below is then a scalar load
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int E = g.E, m = g.m, n = g.n;
+struct GroupLayout {  // byte offsets inside one group's scratch block
+    size_t v2c, c2v, sw, xw, pw, rw, total;
+};
+
+__host__ __device__ inline size_t grp_round(size_t b) { return (b + 255) / 256 * 256; }
+
+__host__ __device__ inline GroupLayout group_layout(const DevGraph& g, size_t tsz) {
+    GroupLayout L;
+    L.v2c = 0;
+    L.c2v = L.v2c + grp_round((size_t)g.E * 64 * tsz);
+    L.sw = L.c2v + grp_round((size_t)g.E * 64 * tsz);
+    L.xw = L.sw + grp_round((size_t)g.m * 8);
+    L.pw = L.xw + grp_round((size_t)g.n * 8);
+    L.rw = L.pw + grp_round((size_t)g.m * 8);
+    L.total = L.rw + grp_round((size_t)g.n_data * 8);
+    return L;
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+template <typename T, int METHOD, int DR, int DC>
+__global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, DecodeArgs a, unsigned char* scratch,
+                                                               size_t group_bytes,
+                                                               const int32_t* __restrict__ rp,
+                                                               const int32_t* __restrict__ ci,
+                                                               const int32_t* __restrict__ cp,
+                                                               const int32_t* __restrict__ ce,
+                                                               const int32_t* __restrict__ ecs,
+                                                               const T* __restrict__ prior) {
+    __shared__ unsigned long long s_bad, s_fail;
+    __shared__ long long s_base;
+    __shared__ int s_qbase;
+    // wave index as a scalar: the graph index loads of the passes are scalar loads
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), tid = threadIdx.x;
+    const int m = g.m, n = g.n, nd = g.n_data;
+    const GroupLayout L = group_layout(g, sizeof(T));
     unsigned long long* counter = reinterpret_cast<unsigned long long*>(scratch);
-    unsigned char* blk = scratch + kLaneHeader + (size_t)blockIdx.x * group_bytes;
-    T* v2c = reinterpret_cast<T*>(blk) + lane;                        // [E][64]
-    T* c2v = v2c + (size_t)E * 64;                                    // [E][64], CSC edge order
-    uint8_t* sbit = reinterpret_cast<uint8_t*>(reinterpret_cast<T*>(blk) + (size_t)2 * E * 64) + lane;  // [m][64]
-    uint8_t* xh = sbit + (size_t)m * 64;                              // [n][64]
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.q_count = (int32_t)a.B;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    int64_t shot = -1;   // identical in every wave (all decisions below are workgroup-uniform per lane)
+    unsigned char* blk = scratch + kGrpHeader + (size_t)blockIdx.x * group_bytes;
+    T* v2c = reinterpret_cast<T*>(blk + L.v2c) + lane;
+    T* c2v = reinterpret_cast<T*>(blk + L.c2v) + lane;
+    uint64_t* sw = reinterpret_cast<uint64_t*>(blk + L.sw);
+    uint64_t* xw = reinterpret_cast<uint64_t*>(blk + L.xw);
+    uint64_t* pw = reinterpret_cast<uint64_t*>(blk + L.pw);
+    uint64_t* rw = reinterpret_cast<uint64_t*>(blk + L.rw);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    int64_t shot = -1;  // slot `lane`'s shot: identical in every wave (all decisions are group-uniform)
     int it = 0;
-    bool need = true;
+    uint64_t need = ~0ull;  // slots to refill (uniform)
     for (;;) {
-        // ---- refill finished slots with the next shots
-        const unsigned long long want = __ballot(need);
-        if (want) {
-            if (threadIdx.x == 0) next_base = (long long)atomicAdd(counter, (unsigned long long)__popcll(want));
+        if (need) {
+            if (tid == 0) s_base = (long long)atomicAdd(counter, (unsigned long long)__popcll(need));
             __syncthreads();
-            if (need) {
-                const long long s2 = next_base + __popcll(want & below);
+            const long long b0 = s_base;
+            if ((need >> lane) & 1) {
+                const long long s2 = b0 + __popcll(need & below);
                 shot = s2 < a.B ? s2 : -1;
                 it = 0;
-                if (shot >= 0) {
-                    for (int i = wv; i < m; i += kLaneWaves) {
-                        int s = a.syn ? (a.syn[shot * m + i] & 1) : 0;
-                        if (a.syn_flags)
-                            for (int e = rp[i]; e < rp[i + 1]; ++e) {
-                                const int j = ci[e];
-                                if (j >= g.n_data) continue;
-                                if ((a.syn_flags & 1) && a.base) s ^= a.base[shot * g.n_data + j] & 1;
-                                if ((a.syn_flags & 2) && a.readout) s ^= a.readout[shot * g.n_data + j] & 1;
-                            }
-                        sbit[(uint32_t)i * 64u] = (uint8_t)s;
-                    }
-                    for (int j = wv; j < n; j += kLaneWaves) {
-                        const T pj = prior[j];
-                        for (int t = cp[j]; t < cp[j + 1]; ++t) v2c[(uint32_t)ce[t] * 64u] = pj;
-                    }
-                }
             }
-            need = false;
+            const uint64_t live = __ballot(((need >> lane) & 1) && shot >= 0);
+            // syndrome words: the refilled slots' bits are replaced in one sweep
+            // (per slot l a coalesced read of its shot's syndrome row)
+            for (int i = tid; i < m; i += kGrpThreads) {
+                uint64_t w = sw[i] & ~need;
+                for (uint64_t rem = live; rem; rem &= rem - 1) {
+                    const int l = __builtin_ctzll(rem);
+                    const long long sl = b0 + __popcll(need & ((1ull << l) - 1ull));
+                    w |= (uint64_t)(a.syn[sl * m + i] & 1) << l;
+                }
+                sw[i] = w;
+            }
         }
         const bool active = shot >= 0;
         if (!__syncthreads_or(active)) break;
+        // every thread read the previous iteration's s_bad before this barrier;
+        // the next atomics come two barriers later
+        if (tid == 0) s_bad = 0;
         ++it;
         const T alpha = alpha_at<T>(it, a.ms_scaling);
-        // Each wave takes kLaneU consecutive checks (or variables) per step and
-        // issues all their loads before using any: kLaneU * DR loads in flight.
-        // Every lane runs the passes, idle ones on their own (unused) slot, so the
-        // control flow below is wave-uniform: scalar branches, no exec masking.
-        {
-            for (int i0 = wv * kLaneU; i0 < m; i0 += kLaneWaves * kLaneU) {  // check pass
-                int e0[kLaneU], d[kLaneU], par[kLaneU];
-                T v[kLaneU][DR];
+        const bool fresh = it == 1;  // first pass of this slot's shot: v2c = priors
+        // Every lane runs the passes, idle slots on garbage, so control flow is
+        // wave-uniform: scalar branches, no exec masking.
+        for (int i0 = wv * kGrpU; i0 < m; i0 += kGrpWaves * kGrpU) {  // check pass
+            int e0[kGrpU], d[kGrpU], par[kGrpU];
+            T v[kGrpU][DR];
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u) {
-                    const int i = i0 + u;
-                    e0[u] = i < m ? rp[i] : 0;
-                    d[u] = i < m ? rp[i + 1] - e0[u] : 0;
-                    par[u] = i < m ? sbit[(uint32_t)i * 64u] : 0;
-                }
+            for (int u = 0; u < kGrpU; ++u) {
+                const int i = i0 + u;
+                e0[u] = i < m ? rp[i] : 0;
+                d[u] = i < m ? rp[i + 1] - e0[u] : 0;
+                // sw is written by this kernel: a volatile (vector) load, never the scalar cache
+                par[u] = i < m ? (int)((*(volatile const uint64_t*)&sw[i] >> lane) & 1ull) : 0;
+            }
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u)
+            for (int u = 0; u < kGrpU; ++u)
 #pragma unroll
-                    for (int t = 0; t < DR; ++t)
-                        if (t < d[u]) v[u][t] = v2c[(uint32_t)(e0[u] + t) * 64u];
+                for (int t = 0; t < DR; ++t)
+                    if (t < d[u]) {
+                        const T mv = v2c[(size_t)(e0[u] + t) * 64];
+                        const T pv = prior[ci[e0[u] + t]];
+                        v[u][t] = fresh ? pv : mv;
+                    }
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u) {
+            for (int u = 0; u < kGrpU; ++u) {
+                if constexpr (METHOD == 1) {
                     T m1 = Big<T>::v, m2 = Big<T>::v;
                     int pu = par[u];
 #pragma unroll
@@ -748,90 +803,187 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
                     for (int t = 0; t < DR; ++t)
                         if (t < d[u]) {
                             const T y = (fabs(v[u][t]) == m1) ? m2a : m1a;
-                            c2v[(uint32_t)ecs[e0[u] + t] * 64u] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
+                            c2v[(size_t)ecs[e0[u] + t] * 64] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
+                        }
+                } else {
+                    T r[DR], fw[DR];
+                    T f = par[u] ? (T)-1 : (T)1;
+#pragma unroll
+                    for (int t = 0; t < DR; ++t)
+                        if (t < d[u]) {
+                            fw[t] = f;
+                            r[t] = (T)2 / ((T)1 + v[u][t]) - (T)1;
+                            f *= r[t];
+                        }
+                    T b = (T)1;
+#pragma unroll
+                    for (int t = DR - 1; t >= 0; --t)
+                        if (t < d[u]) {
+                            const T c = fw[t] * b;
+                            c2v[(size_t)ecs[e0[u] + t] * 64] = ((T)1 - c) / ((T)1 + c);
+                            b *= r[t];
                         }
                 }
             }
         }
         __syncthreads();
-        {
-            for (int j0 = wv * kLaneU; j0 < n; j0 += kLaneWaves * kLaneU) {  // variable pass
-                int t0[kLaneU], d[kLaneU];
-                T c[kLaneU][DC];
+        for (int j0 = wv * kGrpU; j0 < n; j0 += kGrpWaves * kGrpU) {  // column pass
+            int t0[kGrpU], d[kGrpU];
+            T c[kGrpU][DC];
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u) {
-                    const int j = j0 + u;
-                    t0[u] = j < n ? cp[j] : 0;
-                    d[u] = j < n ? cp[j + 1] - t0[u] : 0;
-                }
+            for (int u = 0; u < kGrpU; ++u) {
+                const int j = j0 + u;
+                t0[u] = j < n ? cp[j] : 0;
+                d[u] = j < n ? cp[j + 1] - t0[u] : 0;
+            }
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u)
+            for (int u = 0; u < kGrpU; ++u)
 #pragma unroll
-                    for (int t = 0; t < DC; ++t)
-                        if (t < d[u]) c[u][t] = c2v[(uint32_t)(t0[u] + t) * 64u];  // CSC order: contiguous
+                for (int t = 0; t < DC; ++t)
+                    if (t < d[u]) c[u][t] = c2v[(size_t)(t0[u] + t) * 64];  // CSC order: contiguous
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u) {
-                    const int j = j0 + u;
-                    if (j >= n) continue;
-                    T pre[DC];
-                    T acc = prior[j];
+            for (int u = 0; u < kGrpU; ++u) {
+                const int j = j0 + u;
+                if (j >= n) break;
+                T pre[DC];
+                T acc = prior[j];
+                bool hard;
+                if constexpr (METHOD == 1) {
 #pragma unroll
                     for (int t = 0; t < DC; ++t)
                         if (t < d[u]) {
                             pre[t] = acc;
                             acc += c[u][t];
                         }
-                    xh[(uint32_t)j * 64u] = acc <= (T)0;
-                    if (a.llr_out && active) reinterpret_cast<T*>(a.llr_out)[shot * n + j] = acc;
+                    hard = acc <= (T)0;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < DC; ++t)
+                        if (t < d[u]) {
+                            pre[t] = acc;
+                            acc *= c[u][t];
+                            if (isnan(acc)) acc = (T)1;
+                        }
+                    hard = acc >= (T)1;
+                }
+                const uint64_t hw = __ballot(hard);
+                if (lane == 0) xw[j] = hw;
+                if (a.llr_out && active) {
+                    T* lo = reinterpret_cast<T*>(a.llr_out);
+                    if constexpr (METHOD == 1) lo[shot * n + j] = acc;
+                    else lo[shot * n + j] = (T)log((double)((T)1 / acc));
+                }
+                if constexpr (METHOD == 1) {
                     T suf = (T)0;
 #pragma unroll
                     for (int t = DC - 1; t >= 0; --t)
                         if (t < d[u]) {
-                            v2c[(uint32_t)ce[t0[u] + t] * 64u] = pre[t] + suf;
+                            v2c[(size_t)ce[t0[u] + t] * 64] = pre[t] + suf;
                             suf += c[u][t];
+                        }
+                } else {
+                    T suf = (T)1;
+#pragma unroll
+                    for (int t = DC - 1; t >= 0; --t)
+                        if (t < d[u]) {
+                            v2c[(size_t)ce[t0[u] + t] * 64] = pre[t] * suf;
+                            suf *= c[u][t];
+                            if (isnan(suf)) suf = (T)1;
                         }
                 }
             }
         }
         __syncthreads();
-        bool bad = false;
-        {
-            for (int i0 = wv * kLaneU; i0 < m; i0 += kLaneWaves * kLaneU) {  // syndrome test
+        {  // syndrome test: lane-parallel over checks, 64 slots per word
+            uint64_t bad = 0;
+            for (int i = tid; i < m; i += kGrpThreads) {
+                const int e0 = rp[i], d = rp[i + 1] - e0;
+                uint64_t p = sw[i];
+                int cc[DR];
 #pragma unroll
-                for (int u = 0; u < kLaneU; ++u) {
-                    const int i = i0 + u;
-                    if (i >= m) break;
-                    int par = sbit[(uint32_t)i * 64u];
-                    const int e0 = rp[i], d = rp[i + 1] - e0;
+                for (int t = 0; t < DR; ++t)
+                    if (t < d) cc[t] = ci[e0 + t];
 #pragma unroll
-                    for (int t = 0; t < DR; ++t)
-                        if (t < d) par ^= xh[(uint32_t)ci[e0 + t] * 64u];
-                    bad |= par != 0;
+                for (int t = 0; t < DR; ++t)
+                    if (t < d) p ^= xw[cc[t]];
+                pw[i] = p;
+                bad |= p;
+            }
+            if (bad) atomicOr(&s_bad, (unsigned long long)bad);
+        }
+        __syncthreads();
+        const uint64_t anybad = s_bad;
+        const bool conv = active && !((anybad >> lane) & 1ull);
+        const bool done = conv || (active && it >= a.max_iter);
+        const uint64_t D = __ballot(done);
+        need = D;
+        if (!D) continue;
+        const uint64_t C = __ballot(conv);
+        const uint64_t Q = a.ssf ? (D & ~C) : 0ull;  // BP-unconverged shots -> the SSF queue
+        const uint64_t F = D & ~Q;                   // finalised here
+        if (wv == 0 && done && a.iters) a.iters[shot] = it;
+        if (Q) {
+            if (tid == 0) s_qbase = atomicAdd(a.q_count, __popcll(Q));
+            __syncthreads();
+            const int qb = s_qbase;
+            if (wv == 0 && ((Q >> lane) & 1)) a.q_idx[qb + __popcll(Q & below)] = shot;
+            for (int j = tid; j < n; j += kGrpThreads) {
+                const uint64_t w = xw[j];
+                int r = 0;
+                for (uint64_t rem = Q; rem; rem &= rem - 1, ++r)
+                    a.q_x[(int64_t)(qb + r) * n + j] = (uint8_t)((w >> __builtin_ctzll(rem)) & 1ull);
+            }
+            for (int i = tid; i < m; i += kGrpThreads) {
+                const uint64_t w = pw[i];
+                int r = 0;
+                for (uint64_t rem = Q; rem; rem &= rem - 1, ++r)
+                    a.q_r[(int64_t)(qb + r) * m + i] = (uint8_t)((w >> __builtin_ctzll(rem)) & 1ull);
+            }
+        }
+        if (F) {
+            if (a.x_out)
+                for (int j = tid; j < n; j += kGrpThreads) {
+                    const uint64_t w = xw[j];
+                    for (uint64_t rem = F; rem; rem &= rem - 1) {
+                        const int l = __builtin_ctzll(rem);
+                        a.x_out[readlane64(shot, l) * n + j] = (uint8_t)((w >> l) & 1ull);
+                    }
+                }
+            if (a.corr_out || want_fail) {
+                for (int q = tid; q < nd; q += kGrpThreads) {
+                    uint64_t cw = 0;
+                    for (int b = 0; b < g.fold_blocks; ++b) cw ^= xw[b * nd + q];
+                    uint64_t rword = 0;
+                    for (uint64_t rem = F; rem; rem &= rem - 1) {
+                        const int l = __builtin_ctzll(rem);
+                        const int64_t sl = readlane64(shot, l);
+                        int cb = (int)((cw >> l) & 1ull);
+                        if (a.base) cb ^= a.base[sl * nd + q] & 1;
+                        if (a.corr_out) a.corr_out[sl * nd + q] = (uint8_t)cb;
+                        if (want_fail) rword |= (uint64_t)((a.readout[sl * nd + q] ^ cb) & 1) << l;
+                    }
+                    if (want_fail) rw[q] = rword;
                 }
             }
-        }
-        const unsigned long long bw = __ballot(bad && active);
-        if (lane == 0) bad_w[wv] = bw;
-        __syncthreads();
-        unsigned long long any = 0;
-#pragma unroll
-        for (int w = 0; w < kLaneWaves; ++w) any |= bad_w[w];
-        const bool conv = active && !((any >> lane) & 1);
-        const bool done = conv || (active && it >= a.max_iter);
-        if (done) {  // queue the shot: hard decision, residual syndrome, converged bit
-            for (int j = wv; j < n; j += kLaneWaves) a.q_x[shot * n + j] = xh[(uint32_t)j * 64u];
-            for (int i = wv; i < m; i += kLaneWaves) {
-                int par = sbit[(uint32_t)i * 64u];
-                for (int e = rp[i]; e < rp[i + 1]; ++e) par ^= xh[(uint32_t)ci[e] * 64u];
-                a.q_r[shot * m + i] = (uint8_t)par;
+            if (want_fail) {
+                if (tid == 0) s_fail = 0;
+                __syncthreads();  // rw complete
+                uint64_t fm = 0;
+                for (int r = tid; r < g.k; r += kGrpThreads) {
+                    uint64_t p = 0;
+                    for (int t = g.lz_ptr[r]; t < g.lz_ptr[r + 1]; ++t) p ^= rw[g.lz_idx[t]];
+                    fm |= p;
+                }
+                if (fm & F) atomicOr(&s_fail, (unsigned long long)(fm & F));
+                __syncthreads();
             }
-            if (wv == 0) {
-                a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
-                if (a.iters) a.iters[shot] = it;
+            if (wv == 0 && ((F >> lane) & 1)) {
+                if (a.status) a.status[shot] = (uint8_t)(conv ? 3 : 0);
+                if (a.ssf_steps) a.ssf_steps[shot] = 0;
+                if (a.fail) a.fail[shot] = (uint8_t)(want_fail ? ((s_fail >> lane) & 1ull) : 0);
             }
         }
-        need = done;
-        __syncthreads();  // queue reads of sbit/xh and bad_w reads before the refill
+        __syncthreads();  // every read of s_fail and of the words before the refill
     }
 }
 
@@ -860,7 +1012,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void bp_lane_kernel(DevGraph g, De
 //      hard decision, parity xors; new v2c kept in registers
 //   D  barrier (every state read before any row slot is overwritten)
 //   E  scatter v2c into the rows, barrier
-// Finished shots go to the SSF queue exactly as from bp_lane_kernel (hard
+// Finished shots go to the SSF queue in the byte format of the other BP kernels (hard
 // decision, residual, converged bit); ssf_block_kernel runs SSF and finalises.
 // Pad edges (k >= the column's degree, variables j >= n) point at dummy rows
 // past row m (element m * kMlDRS + lane, so no two lanes of a wave write the
@@ -1167,8 +1319,8 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
     if (placement != 3) {
         // scratch = header (dynamic shot counter) + per-workgroup slices in HBM
         const size_t per_wg = block_slice_bytes(g, sizeof(T), placement);
-        if (!scratch || per_wg == 0 || scratch_bytes <= kLaneHeader) return (int)hipErrorInvalidValue;
-        const long long max_wg = (long long)((scratch_bytes - kLaneHeader) / per_wg);
+        if (!scratch || per_wg == 0 || scratch_bytes <= kGrpHeader) return (int)hipErrorInvalidValue;
+        const long long max_wg = (long long)((scratch_bytes - kGrpHeader) / per_wg);
         // the grid is num_cus * cap workgroups, each owning one slice: at least
         // one slice per CU (block_scratch_bytes sizes 4 per CU)
         if (max_wg < num_cus) return (int)hipErrorOutOfMemory;
@@ -1183,7 +1335,7 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
         if (const char* wv = getenv("QDEC_BLOCK_WG_PER_CU"))
             if (atoi(wv) > 0) cap = std::min((int)(max_wg / num_cus), atoi(wv));
         a.work_ctr = static_cast<unsigned long long*>(scratch);
-        gs = reinterpret_cast<T*>(static_cast<unsigned char*>(scratch) + kLaneHeader);
+        gs = reinterpret_cast<T*>(static_cast<unsigned char*>(scratch) + kGrpHeader);
         const hipError_t e0 = hipMemsetAsync(a.work_ctr, 0, sizeof(unsigned long long), stream);
         if (e0 != hipSuccess) return (int)e0;
     }
@@ -1266,112 +1418,119 @@ static int launch_lds(const DevGraph& g, const DecodeArgs& a, int num_cus, hipSt
     return launch_lds_typed<16>(g, a, num_cus, stream);
 }
 
-// ---------------------------------------------------------------- shot-lane launch
-template <typename T, int DR, int DC>
-static int launch_lane_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, void* scratch,
-                             size_t scratch_bytes) {
-    const size_t group_bytes = (64 * lane_slot_bytes(g, sizeof(T)) + 255) / 256 * 256;
-    // tail of the scratch: HBM shot state of the finalize/SSF workgroups when it
+// ---------------------------------------------------------------- slot-group launch
+static size_t group_scratch_budget() {
+    const char* v = getenv("QDEC_GROUP_SCRATCH_MB");
+    const long long mb = v ? atoll(v) : 65536;  // 64 GiB of the 288 GB HBM
+    return (size_t)std::max(64ll, mb) << 20;
+}
+
+// Groups in flight: up to 2 per CU (the kernel's occupancy), capped by the
+// scratch budget and by the batch (every slot should see >= 4 shots, so the
+// tail of a launch stays short and small test batches stay small).
+static int64_t group_count(const DevGraph& g, size_t tsz, int num_cus, int64_t B) {
+    const size_t per = group_layout(g, tsz).total;
+    int64_t c = std::min<int64_t>((int64_t)num_cus * 2, (int64_t)(group_scratch_budget() / per));
+    c = std::min<int64_t>(c, (B + 255) / 256);
+    return std::max<int64_t>(c, 1);
+}
+
+// The slot-group kernel takes min-sum and product-sum graphs whose messages do
+// not fit the small-graph LDS budget (row degree <= 16, column degree <= 8, the
+// syndrome given directly).  QDEC_GROUP_KERNEL=0 disables it (workgroup kernel
+// with HBM message slices), =1 forces it on any graph within those degrees.
+// For fp32 min-sum graphs the LDS-resident kernel (bp_ms_lds_kernel) keeps
+// precedence unless the group kernel is forced.
+bool group_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a) {
+    if (g.max_rdeg > 16 || g.max_cdeg > 8 || !a.syn || a.syn_flags) return false;
+    (void)method;
+    const char* opt = getenv("QDEC_GROUP_KERNEL");
+    if (opt && opt[0] == '0') return false;
+    if (opt && opt[0] == '1') return true;
+    return block_placement(g, precision == 1 ? 4 : 8) != 3;
+}
+
+template <typename T, int METHOD, int DR, int DC>
+static int launch_group_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, void* scratch,
+                              size_t scratch_bytes) {
+    const size_t gb = group_layout(g, sizeof(T)).total;
+    // tail of the scratch: HBM shot state of the SSF/finalize workgroups when it
     // does not fit LDS (kFinPerCu workgroups per CU)
-    const bool fin_hbm = block_placement(g, sizeof(T)) == 0;
+    const bool fin_hbm = a.ssf && block_placement(g, sizeof(T)) == 0;
     const size_t fin_bytes = fin_hbm ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
-    if (scratch_bytes <= fin_bytes + kLaneHeader) return (int)hipErrorOutOfMemory;
+    if (!scratch || scratch_bytes < fin_bytes + kGrpHeader + gb) return (int)hipErrorOutOfMemory;
     unsigned char* base = static_cast<unsigned char*>(scratch);
     unsigned char* fin_state = fin_hbm ? base + (scratch_bytes - fin_bytes) : nullptr;
-    const int64_t max_groups = (int64_t)((scratch_bytes - fin_bytes - kLaneHeader) / group_bytes);
+    const int64_t max_groups = (int64_t)((scratch_bytes - fin_bytes - kGrpHeader) / gb);
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_lane_kernel<T, DR, DC>, 64 * kLaneWaves, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_group_kernel<T, METHOD, DR, DC>,
+                                                                kGrpThreads, 0);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
     int64_t grid = std::min<int64_t>((int64_t)num_cus * per_cu, max_groups);
-    grid = std::min<int64_t>(grid, (a.B + 63) / 64);
+    grid = std::min<int64_t>(grid, group_count(g, sizeof(T), num_cus, a.B));
     if (grid <= 0) return (int)hipErrorOutOfMemory;
     e = hipMemsetAsync(base, 0, sizeof(unsigned long long), stream);  // shot counter
     if (e != hipSuccess) return (int)e;
+    if (a.ssf) {
+        if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+        e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
+        if (e != hipSuccess) return (int)e;
+    }
     record_ev(a, 0, stream);
-    hipLaunchKernelGGL((bp_lane_kernel<T, DR, DC>), dim3((unsigned)grid), dim3(64 * kLaneWaves), 0, stream, g, a,
-                       base, group_bytes, g.row_ptr, g.col_idx, g.col_ptr, g.col_edge, g.edge_csc,
-                       reinterpret_cast<const T*>(g.prior[1][sizeof(T) == 4 ? 1 : 0]));
-    hipError_t le = hipGetLastError();
+    hipLaunchKernelGGL((bp_group_kernel<T, METHOD, DR, DC>), dim3((unsigned)grid), dim3(kGrpThreads), 0, stream, g, a,
+                       base, gb, g.row_ptr, g.col_idx, g.col_ptr, g.col_edge, g.edge_csc,
+                       reinterpret_cast<const T*>(g.prior[METHOD][sizeof(T) == 4 ? 1 : 0]));
+    const hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;
-    const int rc = fin_hbm ? launch_block2(ssf_block_kernel, kCtrl, a.B, num_cus, stream, g, a, fin_state, kFinPerCu)
-                           : launch_ssf_fin(g, a, num_cus, stream);
+    int rc = 0;
+    if (a.ssf)
+        rc = fin_hbm ? launch_block2(ssf_block_kernel, kCtrl, a.B, num_cus, stream, g, a, fin_state, kFinPerCu)
+                     : launch_ssf_fin(g, a, num_cus, stream);
     record_ev(a, 2, stream);
     return rc;
 }
 
-size_t lane_slot_bytes(const DevGraph& g, size_t tsz) {
-    return (size_t)2 * g.E * tsz + (size_t)g.m + (size_t)g.n;
+template <typename T, int METHOD>
+static int launch_group_shape(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, void* scratch,
+                              size_t scratch_bytes) {
+    const bool r8 = g.max_rdeg <= 8, c4 = g.max_cdeg <= 4;
+    if (r8) return c4 ? launch_group_typed<T, METHOD, 8, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
+                      : launch_group_typed<T, METHOD, 8, 8>(g, a, num_cus, stream, scratch, scratch_bytes);
+    return c4 ? launch_group_typed<T, METHOD, 16, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
+              : launch_group_typed<T, METHOD, 16, 8>(g, a, num_cus, stream, scratch, scratch_bytes);
 }
 
-// Workgroups of the lane kernel in flight (its occupancy is 2 per CU: 8 waves of
-// <= 128 VGPRs), capped by the HBM scratch budget.
-static size_t lane_groups(const DevGraph& g, size_t tsz, int num_cus);
-
-// Shot-lane kernel or workgroup kernel for a min-sum graph whose messages
-// spill to HBM.  QDEC_LANE_KERNEL=1 forces the lane kernel, =0 (the default)
-// the workgroup kernel; =auto picks the lane kernel when the per-shot state fits
-// LDS (the finalize stays in LDS) and the batch gives every slot >= 4 shots, so
-// one slow shot does not hold its 63 lane-mates for long.  Since the workgroup
-// kernel got its unrolled min-sum loops and dynamic shot counter it is faster at
-// low iteration counts (C4 at p = 0.01: 581 k vs 313 k shots/s) and the lane
-// kernel only wins when nearly every shot runs max_iter.
-bool lane_kernel_applies(const DevGraph& g, int method, int precision, int64_t B, int num_cus) {
-    if (method != 1 || g.max_rdeg > 16 || g.max_cdeg > 8) return false;
+size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, const DecodeArgs& a) {
     const size_t tsz = precision == 1 ? 4 : 8;
-    const int placement = block_placement(g, tsz);
-    if (placement == 3) return false;
-    const char* opt = getenv("QDEC_LANE_KERNEL");
-    if (opt && opt[0] == '1') return true;
-    if (!opt || strcmp(opt, "auto") != 0) return false;
-    if (placement != 2) return false;
-    return B >= 4 * 64 * (int64_t)lane_groups(g, tsz, num_cus);
-}
-
-static size_t lane_scratch_budget() {
-    const char* v = getenv("QDEC_LANE_SCRATCH_MB");
-    const long long mb = v ? atoll(v) : 24576;  // 24 GiB of the 288 GB HBM
-    return (size_t)std::max(64ll, mb) << 20;
-}
-
-static size_t lane_groups(const DevGraph& g, size_t tsz, int num_cus) {
-    const size_t per_group = (64 * lane_slot_bytes(g, tsz) + 255) / 256 * 256;
-    return std::max<size_t>(1, std::min<size_t>(lane_scratch_budget() / per_group, (size_t)num_cus * 2));
-}
-
-size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, int64_t B) {
-    if (lane_kernel_applies(g, method, precision, B, num_cus)) {
-        const size_t tsz = precision == 1 ? 4 : 8;
-        const size_t per_group = (64 * lane_slot_bytes(g, tsz) + 255) / 256 * 256;
-        const size_t fin = block_placement(g, tsz) == 0 ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
-        return kLaneHeader + lane_groups(g, tsz, num_cus) * per_group + fin;
+    if (group_kernel_applies(g, method, precision, a) && !(lds_kernel_applies(g, method, precision, a) &&
+                                                           !(getenv("QDEC_GROUP_KERNEL") &&
+                                                             getenv("QDEC_GROUP_KERNEL")[0] == '1'))) {
+        const size_t fin = (a.ssf && block_placement(g, tsz) == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g)
+                                                                  : 0;
+        return kGrpHeader + (size_t)group_count(g, tsz, num_cus, a.B) * group_layout(g, tsz).total + fin;
     }
-    const size_t tsz = precision == 1 ? 4 : 8;
     const int placement = block_placement(g, tsz);
     if (placement == 3) return 0;
     // shot-counter header + up to 4 workgroup slices per CU
-    return kLaneHeader + (size_t)num_cus * 4 * block_slice_bytes(g, tsz, placement);
+    return kGrpHeader + (size_t)num_cus * 4 * block_slice_bytes(g, tsz, placement);
 }
 
 int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
                         hipStream_t stream, void* scratch, size_t scratch_bytes) {
     if (a.B <= 0) return 0;
     if (a.ssf && g.n_gen <= 0) return (int)hipErrorInvalidValue;
-    if (lane_kernel_applies(g, method, precision, a.B, num_cus)) {
-        if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r || !scratch) return (int)hipErrorInvalidValue;
-        const bool r8 = g.max_rdeg <= 8, c4 = g.max_cdeg <= 4;
+    const char* gopt = getenv("QDEC_GROUP_KERNEL");
+    const bool lds = lds_kernel_applies(g, method, precision, a);
+    if (group_kernel_applies(g, method, precision, a) && !(lds && !(gopt && gopt[0] == '1'))) {
         if (precision == 1)
-            return r8 ? (c4 ? launch_lane_typed<float, 8, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
-                            : launch_lane_typed<float, 8, 8>(g, a, num_cus, stream, scratch, scratch_bytes))
-                      : (c4 ? launch_lane_typed<float, 16, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
-                            : launch_lane_typed<float, 16, 8>(g, a, num_cus, stream, scratch, scratch_bytes));
-        return r8 ? (c4 ? launch_lane_typed<double, 8, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
-                        : launch_lane_typed<double, 8, 8>(g, a, num_cus, stream, scratch, scratch_bytes))
-                  : (c4 ? launch_lane_typed<double, 16, 4>(g, a, num_cus, stream, scratch, scratch_bytes)
-                        : launch_lane_typed<double, 16, 8>(g, a, num_cus, stream, scratch, scratch_bytes));
+            return method == 1 ? launch_group_shape<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
+                               : launch_group_shape<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
+        return method == 1 ? launch_group_shape<double, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
+                           : launch_group_shape<double, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
     }
-    if (lds_kernel_applies(g, method, precision, a)) return launch_lds(g, a, num_cus, stream);
+    if (lds) return launch_lds(g, a, num_cus, stream);
     if (precision == 1)
         return method == 1 ? launch_block_typed<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_block_typed<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);

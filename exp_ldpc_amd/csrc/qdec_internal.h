@@ -103,7 +103,13 @@ struct DevGraph {
     const uint32_t* g_ient;
     // logicals (fused failure check)
     int k, lz_words;
-    const uint64_t* lz;           // [k][lz_words]    bit q%64 of word q/64
+    const uint64_t* lz;           // [k][lz_words]    bit q%64 of word q/64 (nullptr when too large)
+    // the same logicals as CSR supports over data qubits (always set with k > 0);
+    // lz_sparse: the workgroup finalize tests logicals on their supports (nnz small
+    // against k * lz_words) instead of by dense words
+    const int32_t* lz_ptr;        // [k+1]
+    const int32_t* lz_idx;        // [nnz]
+    int lz_sparse;
 };
 
 struct DecodeArgs {
@@ -178,10 +184,9 @@ int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs
 int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
                         hipStream_t stream, void* scratch, size_t scratch_bytes);
 int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream);
-size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, int64_t B);
-bool lane_kernel_applies(const DevGraph& g, int method, int precision, int64_t B, int num_cus);
+size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, const DecodeArgs& a);
+bool group_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a);
 bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a);
-size_t lane_slot_bytes(const DevGraph& g, size_t tsz);
 int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,
                           uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
                           uint8_t* syn, uint8_t* readout, int num_cus, hipStream_t stream);

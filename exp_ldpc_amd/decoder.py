@@ -115,11 +115,22 @@ class Decoder:
         self.has_flip_sets = True
 
     def set_logicals(self, lz) -> None:
-        lz = np.ascontiguousarray(np.asarray(lz.todense() if sp.issparse(lz) else lz) % 2, dtype=np.uint8)
-        if lz.ndim != 2 or lz.shape[1] != self.n_data:
+        """Logical operators (k x n_data, dense or scipy sparse) for the fused
+        failure check; handed over as CSR supports (qd_graph_set_logicals_csr),
+        so codes with thousands of sparse logicals never build a dense k x n
+        array."""
+        L = sp.csr_matrix(lz if sp.issparse(lz) else np.asarray(lz) % 2)
+        if L.ndim != 2 or L.shape[1] != self.n_data:
             raise ValueError("logicals must be k x n_data")
-        _abi.check(self._lib.qd_graph_set_logicals(self._handle, lz.shape[0], _abi.ptr(lz)), "qd_graph_set_logicals")
-        self.k = lz.shape[0]
+        L.sum_duplicates()
+        L.data %= 2
+        L.eliminate_zeros()
+        L.sort_indices()
+        ptr = np.ascontiguousarray(L.indptr, dtype=np.int32)
+        idx = np.ascontiguousarray(L.indices, dtype=np.int32)
+        _abi.check(self._lib.qd_graph_set_logicals_csr(self._handle, L.shape[0], _abi.ptr(ptr), _abi.ptr(idx)),
+                   "qd_graph_set_logicals_csr")
+        self.k = L.shape[0]
 
     def _params(self, syn_flags: int = 0, ssf: bool | None = None) -> _abi.QdParams:
         return _abi.QdParams(self.max_iter, self.method, self.precision,
@@ -241,7 +252,10 @@ class Decoder:
     def set_ssf_stream(self, stream) -> None:
         """Run the SSF kernel of later decode_device calls on `stream` (a torch
         stream or a raw hipStream_t; None = the decode's own stream); see
-        qd_graph_set_ssf_stream: the caller synchronises with that stream."""
+        qd_graph_set_ssf_stream: the caller synchronises with that stream.
+        The handle's workspace is single-buffered, so this handle's next
+        decode still waits for the SSF kernel: overlap happens only across
+        handles (e.g. one Decoder per p point)."""
         raw = None if stream is None else int(getattr(stream, "cuda_stream", stream))
         _abi.check(self._lib.qd_graph_set_ssf_stream(self._handle, C.c_void_p(raw)), "qd_graph_set_ssf_stream")
 

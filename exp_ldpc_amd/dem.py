@@ -187,7 +187,17 @@ def storage_experiment_dem(hz, lz, rounds: int, p: float, pm: float | None = Non
                  one the rewriter places at the end of the REPEAT body (block t+1);
       then the readout flips (block R).  R = 0 has one data event and the readout.
     A data X error in slot t flips every later syndrome and the readout, so it
-    fires only detector block t and the observables."""
+    fires only detector block t and the observables.
+
+    Deviation from the reference at R >= 2 (unpinned: Stim is absent): the
+    reference's bpd_detector decodes Stim's full circuit DEM
+    (_experiment.py:174,186), which also holds the X-check detectors of the
+    REPEAT body (storage_sim.py:156-157) and keeps X, Y and Z faults as separate
+    columns, so Y errors couple the two sectors there.  This DEM is the Z sector
+    only, with X and Y merged into one column of prior 2p/3 per event; for
+    R <= 1 the two sectors do not interact on the Z detectors the decoder sees.
+    At R >= 2 the GPU bpd_detector therefore solves this Z-sector BP problem,
+    not Stim's two-sector one."""
     if rounds < 0:
         raise ValueError("rounds must be >= 0")
     pm = p if pm is None else pm

@@ -413,16 +413,24 @@ def _load_checkpoint(path):
     import pandas as pd
     if not path or not os.path.exists(path) or os.path.getsize(path) == 0:
         return {}
-    df = pd.read_csv(path, float_precision="round_trip")
+    try:
+        df = pd.read_csv(path, float_precision="round_trip", dtype={"config_fp": str})
+    except Exception:  # unparseable file: nothing is reused (the next append sets it aside)
+        return {}
     if "config_fp" not in df.columns:  # rows without a fingerprint are never reused
         return {}
-    return {(float(r["p_ph"]), str(r["config_fp"])): r.to_dict() for _, r in df.iterrows()}
+    return {(float(r["p_ph"]), str(r["config_fp"])): r.to_dict() for _, r in df.iterrows()
+            if isinstance(r["config_fp"], str)}
 
 
-def _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, samples, point_index) -> str:
+def _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, samples, point_index,
+                        noise=None) -> str:
     """Everything a point's failure count depends on besides p: the check
-    matrices and logicals, the decoder configuration, and the sampler stream
-    (seed, point index = Philox stream id, sample count)."""
+    matrices and logicals, the decoder configuration, the sampler stream
+    (seed, point index = Philox stream id, sample count) and the point's noise
+    configuration ``noise = (noise model, noise_model_args(p), data prior,
+    measurement prior)``: the sampler's event probabilities and the BP priors
+    are built from exactly those."""
     import hashlib
     h = hashlib.sha1()
     for M in (code.checks.x, code.checks.z, code.logicals.x, code.logicals.z):
@@ -433,7 +441,42 @@ def _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, sam
         h.update(np.ascontiguousarray(A.indices, dtype=np.int64).tobytes())
     h.update(repr((int(rounds), str(mode), sorted((k, str(v)) for k, v in bp_osd_options.items()), str(precision),
                    int(seed), int(samples), int(point_index))).encode())
+    if noise is not None:
+        model, model_args, dp, mp = noise
+        name = f"{getattr(model, '__module__', '')}.{getattr(model, '__qualname__', repr(model))}"
+        h.update(repr((name, sorted((str(k), repr(v)) for k, v in dict(model_args).items()))).encode())
+        for prior in (dp, mp):
+            h.update(np.ascontiguousarray(np.atleast_1d(np.asarray(prior, dtype=np.float64))).tobytes())
+            h.update(b"|")
     return h.hexdigest()[:16]
+
+
+def _append_checkpoint_row(path, point) -> None:
+    """Append one finished point to the checkpoint CSV.  A file written with a
+    different column set (an older format, other decoder options) is rewritten
+    with the union of the columns first, so every row stays parseable and the
+    sweep stays resumable (missing cells are empty)."""
+    import pandas as pd
+    row = pd.DataFrame.from_records([point])
+    if not os.path.exists(path) or os.path.getsize(path) == 0:
+        row.to_csv(path, mode="w", header=True, index=False, float_format="%.17g")
+        return
+    with open(path) as f:
+        header = f.readline().rstrip("\n").split(",")
+    if header == list(row.columns):
+        row.to_csv(path, mode="a", header=False, index=False, float_format="%.17g")
+        return
+    try:
+        old = pd.read_csv(path, float_precision="round_trip", dtype={"config_fp": str})
+    except Exception:  # unreadable (e.g. rows wider than their header): keep it aside, start afresh
+        os.replace(path, path + ".unreadable")
+        row.to_csv(path, mode="w", header=True, index=False, float_format="%.17g")
+        return
+    cols = list(old.columns) + [c for c in row.columns if c not in old.columns]
+    merged = pd.concat([old.reindex(columns=cols), row.reindex(columns=cols)], ignore_index=True)
+    tmp = path + ".tmp"
+    merged.to_csv(tmp, mode="w", header=True, index=False, float_format="%.17g")
+    os.replace(tmp, path)
 
 
 def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_prior, *, gpus: int | None = None,
@@ -461,16 +504,18 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
     x_steps, z_steps = _steps(code.checks)
     data = []
     for pi, p_ph in enumerate(p_values):
-        fp = _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, samples, pi)
+        nm_args = noise_model_args(p_ph)
+        dp = data_prior(p_ph, x_steps, z_steps)
+        mp = meas_prior(p_ph, x_steps, z_steps)
+        fp = _config_fingerprint(code, rounds, mode, bp_osd_options, precision, seed, samples, pi,
+                                 noise=(noise_model, nm_args, dp, mp))
         prev = done.get((float(p_ph), fp))
         if prev is not None:
             data.append(prev)
             continue
         t0 = time.perf_counter()
-        nm = noise_model(**noise_model_args(p_ph))
+        nm = noise_model(**nm_args)
         sim = build_storage_simulation(rounds, nm, code, use_x_logicals=False)
-        dp = data_prior(p_ph, x_steps, z_steps)
-        mp = meas_prior(p_ph, x_steps, z_steps)
         pipes = [BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision, noise=nm)
                  for d in range(ndev)]
         per = math.ceil(samples / ndev)
@@ -513,9 +558,7 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
         point["config_fp"] = fp
         data.append(point)
         if checkpoint:
-            row = pd.DataFrame.from_records([point])
-            new_file = not os.path.exists(checkpoint) or os.path.getsize(checkpoint) == 0
-            row.to_csv(checkpoint, mode="a", header=new_file, index=False, float_format="%.17g")
+            _append_checkpoint_row(checkpoint, point)
     return pd.DataFrame.from_records(data)
 
 

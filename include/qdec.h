@@ -79,6 +79,13 @@ int qd_graph_set_flipsets(qd_graph* g, int32_t n_gen, const int32_t* gen_ptr, co
  * _experiment.py:209). */
 int qd_graph_set_logicals(qd_graph* g, int32_t k, const uint8_t* lz);
 
+/* The same logicals as a CSR over data qubits (row r = the support of logical r,
+ * lz_ptr[k+1], lz_idx[nnz] in [0, n_data), duplicates cancel mod 2).  For codes
+ * with many sparse logicals (the PSL(2,16) Cayley-graph LP code of config 5:
+ * k = 4080 of weight 3, n = 53,040) where the dense k x n_data form is hundreds
+ * of MB; the workgroup kernels then test each logical on its support only. */
+int qd_graph_set_logicals_csr(qd_graph* g, int32_t k, const int32_t* lz_ptr, const int32_t* lz_idx);
+
 /* Per-column error probabilities (ldpc `error_rate` broadcast / `channel_probs`;
  * reference call sites _experiment.py:23-27, 37-40, 74-77, 106-113).  Converted
  * on the host to the ldpc initial messages log((1-p)/p) (min-sum) and p/(1-p)
@@ -162,11 +169,13 @@ int qd_graph_set_timing(qd_graph* g, int32_t capacity);
 
 /* Route the SSF kernel of later qd_decode_batch_device calls (wave-kernel graphs)
  * to `ssf_stream` (hipStream_t; NULL = the decode's own stream, the default):
- * it runs behind an event recorded after the BP kernel on the decode stream, so
- * a following BP launch on that stream overlaps it.  Outputs the SSF stage
- * writes (status, ssf_steps, fail, x/corr of BP-failed shots) are complete when
- * `ssf_stream` has passed that point; the caller synchronises with it.  The
- * handle's next decode waits for this SSF kernel (workspace chain).  Replaces
+ * it runs behind an event recorded after the BP kernel on the decode stream.
+ * Outputs the SSF stage writes (status, ssf_steps, fail, x/corr of BP-failed
+ * shots) are complete when `ssf_stream` has passed that point; the caller
+ * synchronises with it.  The handle's SSF queue and control block are single-
+ * buffered, so the handle's next decode waits for this SSF kernel (workspace
+ * chain): on ONE handle a following BP launch never overlaps the previous SSF;
+ * overlap is only possible between decodes on different handles.  Replaces
  * nothing in the reference (its decode is one synchronous call per shot). */
 int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);

@@ -74,6 +74,13 @@ class OracleLib:
             gp = gi = None
             ng = 0
         k = 0
+        lz_sparse = None
+        if lz is not None and sp.issparse(lz):
+            # sparse logicals (thousands of them on the config-5 code): the C loop
+            # is skipped and the check any(Lz (readout ^ corr)) (_experiment.py:209)
+            # is evaluated below on the oracle's own corrections
+            lz_sparse = sp.csr_matrix(lz)
+            lz = None
         if lz is not None:
             lz = np.ascontiguousarray(np.asarray(lz) % 2, dtype=np.uint8)
             k = lz.shape[0]
@@ -94,6 +101,9 @@ class OracleLib:
                                        {"brute": 0, "fast": 1}[ssf_impl], int(nthreads))
         if rc != 0:
             raise ValueError(f"qdo_decode_batch failed with status {rc}")
+        if lz_sparse is not None and readout is not None:
+            resid = sp.csr_matrix((readout ^ out["corr"]) & 1)
+            out["fail"] = ((lz_sparse @ resid.T).toarray() % 2).any(axis=0).astype(np.uint8)
         return out
 
     def sample_storage(self, Hz, rounds, p_data, p_meas, seed, stream, shot0, B, nthreads=0):

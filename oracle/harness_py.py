@@ -63,16 +63,12 @@ def single_shot_corrections(orc, Hz, rounds, raw_history, readout, bp_osd_option
     return ((final + acc) % 2).astype(np.uint8)  # :60
 
 
-def spacetime_bposd_corrections(orc, Hz, rounds, spacetime_syndrome, bp_osd_options, priors, precision="f32"):
-    """BPOSDCorrect.readout_correction (_experiment.py:62-83) for a batch:
-    bposd on H_st (SpacetimeCode, spacetime_code.py:46-75, intended (R+1)-copy
-    block diagonal) with data/measurement priors, then final_correction = XOR
-    of the R+1 data blocks (spacetime_code.py:81-84).  spacetime_syndrome is the
-    differenced syndrome of spacetime_code.py:98-119, uint8[B, (R+1) m]."""
-    data_prior, meas_prior = priors
+def _spacetime_matrix(Hz, R, data_prior, meas_prior):
+    """SpacetimeCode (spacetime_code.py:46-75, the intended (R+1)-copy block
+    diagonal) and its channel prior with data / measurement columns set by their
+    true ranges (_experiment.py:74-76 / :105-107)."""
     Hz = sp.csr_matrix(Hz)
     m, n = Hz.shape
-    R = rounds
     blocks = sp.block_diag([Hz] * (R + 1), format="csr")
     if R > 0:
         M = sp.lil_matrix(((R + 1) * m, R * m), dtype=np.uint8)
@@ -86,11 +82,51 @@ def spacetime_bposd_corrections(orc, Hz, rounds, spacetime_syndrome, bp_osd_opti
     prior = np.empty(Hst.shape[1])
     prior[:(R + 1) * n] = data_prior
     prior[(R + 1) * n:] = meas_prior
-    x = bposd(orc, Hst, prior, spacetime_syndrome, **_opts(bp_osd_options, precision))
+    return Hst, prior
+
+
+def _fold(x, n, R):
+    """SpacetimeCode.final_correction (spacetime_code.py:81-84): XOR of the R+1
+    data blocks."""
     fold = np.zeros((x.shape[0], n), np.uint8)
     for t in range(R + 1):
         fold ^= x[:, t * n:(t + 1) * n]
     return fold
+
+
+def spacetime_bposd_corrections(orc, Hz, rounds, spacetime_syndrome, bp_osd_options, priors, precision="f32"):
+    """BPOSDCorrect.readout_correction (_experiment.py:62-83) for a batch:
+    bposd on H_st (SpacetimeCode, spacetime_code.py:46-75, intended (R+1)-copy
+    block diagonal) with data/measurement priors, then final_correction = XOR
+    of the R+1 data blocks (spacetime_code.py:81-84).  spacetime_syndrome is the
+    differenced syndrome of spacetime_code.py:98-119, uint8[B, (R+1) m]."""
+    data_prior, meas_prior = priors
+    n = Hz.shape[1]
+    Hst, prior = _spacetime_matrix(Hz, rounds, data_prior, meas_prior)
+    x = bposd(orc, Hst, prior, spacetime_syndrome, **_opts(bp_osd_options, precision))
+    return _fold(x, n, rounds)
+
+
+def hybrid_corrections(orc, Hz, rounds, spacetime_syndrome, readout, bp_osd_options, priors, precision="f32"):
+    """BPOSDHybridCorrect.readout_correction (_experiment.py:115-126) for a batch.
+
+    Stage 1 is ldpc's bp_decoder on H_st (:110-113): BP only, its hard decision
+    whether or not BP converged (.decode returns bp_decoding), folded onto the
+    data qubits (:117-118).  The readout is corrected with it (:121), re-syndromed
+    on Hz (:124), and stage 2 is bposd_decoder(Hz, error_rate=data_prior) (:96-100,
+    :125).  Returns uint8[B, n]: stage-2 correction + stage-1 fold (:126)."""
+    data_prior, meas_prior = priors
+    Hz = sp.csr_matrix(Hz)
+    n = Hz.shape[1]
+    Hst, prior = _spacetime_matrix(Hz, rounds, data_prior, meas_prior)
+    kw = _opts(bp_osd_options, precision)
+    out = orc.decode(Hst, prior, np.ascontiguousarray(spacetime_syndrome, dtype=np.uint8), method=kw["bp_method"],
+                     precision=precision, max_iter=kw["max_iter"], ms_scaling=kw["ms_scaling"], want_llr=False)
+    stage1 = _fold(out["x"], n, rounds)  # :117-118
+    rd = (stage1 + readout) % 2  # :121
+    syndrome = (Hz @ rd.T).T % 2  # :124
+    final = bposd(orc, Hz, np.full(n, data_prior), syndrome.astype(np.uint8), **kw)  # :125, error_rate=data_prior
+    return ((final + stage1) % 2).astype(np.uint8)  # :126
 
 
 def logical_failures(Lz, readout, corr):

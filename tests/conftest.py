@@ -25,6 +25,16 @@ def load_checks(name):
     return csr("hx"), csr("hz")
 
 
+def load_logicals(name):
+    """(Lx, Lz) CSR from tests/golden/<name>_logicals.npz."""
+    d = np.load(os.path.join(GOLDEN, f"{name}_logicals.npz"))
+
+    def csr(p):
+        return sp.csr_matrix((np.ones(d[p + "_indices"].size, np.uint8), d[p + "_indices"], d[p + "_indptr"]),
+                             shape=tuple(d[p + "_shape"]))
+    return csr("lx"), csr("lz")
+
+
 def load_code(name):
     from exp_ldpc_amd.codes import read_quantum_code
     with open(os.path.join(GOLDEN, f"{name}.qecc")) as f:

@@ -132,3 +132,47 @@ def test_sharding_arithmetic():
             lo = step_shot0(s, 4, r, 5)
             seen.update(range(lo, lo + 5))
     assert seen == set(range(60))
+
+
+def test_checkpoint_fingerprint_covers_noise_configuration():
+    """A restarted sweep must not reuse a row computed under another noise model
+    argument (pm), prior function or noise model."""
+    from exp_ldpc_amd.codes import QuantumCode, QuantumCodeChecks
+    from exp_ldpc_amd.experiment import _config_fingerprint
+    from exp_ldpc_amd.noise_model import depolarizing_noise, circuit_noise
+    hx, hz = load_checks("hgp_12_3_4_s1234")
+    code = QuantumCode(QuantumCodeChecks(hx, hz))
+    opts = {"max_iter": 30, "bp_method": "ms"}
+    base = (code, 0, "bpssf", opts, "f64", 5, 4000, 0)
+    p = 0.01
+    fp = lambda model, args, dp, mp: _config_fingerprint(*base, noise=(model, args, dp, mp))
+    ref = fp(depolarizing_noise, dict(p=p, pm=p), 2 * p / 3, 2 * p / 3)
+    assert ref == fp(depolarizing_noise, dict(pm=p, p=p), 2 * p / 3, 2 * p / 3)  # order-free
+    assert ref != fp(depolarizing_noise, dict(p=p, pm=2 * p), 2 * p / 3, 2 * p / 3)
+    assert ref != fp(depolarizing_noise, dict(p=p, pm=p), p, 2 * p / 3)
+    assert ref != fp(depolarizing_noise, dict(p=p, pm=p), 2 * p / 3, p)
+    assert ref != fp(circuit_noise, dict(p=p, pm=p), 2 * p / 3, 2 * p / 3)
+    assert ref != _config_fingerprint(*base)  # rows fingerprinted without noise are not reused either
+
+
+def test_checkpoint_append_keeps_file_parseable(tmp_path):
+    """Rows with a different column set (older format, other decoder options)
+    are merged under a union header, so the next restart can read the CSV."""
+    import pandas as pd
+    from exp_ldpc_amd.experiment import _append_checkpoint_row, _load_checkpoint
+    ck = str(tmp_path / "sweep.csv")
+    pd.DataFrame.from_records([{"p_ph": 0.01, "failures": 3, "samples": 100}]).to_csv(ck, index=False)  # old format
+    _append_checkpoint_row(ck, {"p_ph": 0.02, "failures": 5, "samples": 100, "precision": "f64", "config_fp": "ab"})
+    _append_checkpoint_row(ck, {"p_ph": 0.03, "failures": 7, "samples": 100, "precision": "f64", "config_fp": "cd"})
+    _append_checkpoint_row(ck, {"p_ph": 0.04, "failures": 9, "samples": 100, "precision": "f64", "config_fp": "ef",
+                                "osd_order": 7})
+    df = pd.read_csv(ck, float_precision="round_trip")
+    assert list(df["p_ph"]) == [0.01, 0.02, 0.03, 0.04] and list(df["failures"]) == [3, 5, 7, 9]
+    assert "osd_order" in df.columns and df["osd_order"].isna().sum() == 3
+    rows = _load_checkpoint(ck)
+    assert set(rows) == {(0.02, "ab"), (0.03, "cd"), (0.04, "ef")}
+    with open(ck, "a") as f:  # a corrupt tail: loading reuses nothing, the next append sets the file aside
+        f.write("1,2,3,4,5,6,7,8,9,10,11\n")
+    assert _load_checkpoint(ck) == {}
+    _append_checkpoint_row(ck, {"p_ph": 0.05, "failures": 1, "samples": 100, "precision": "f64", "config_fp": "gh"})
+    assert set(_load_checkpoint(ck)) == {(0.05, "gh")}

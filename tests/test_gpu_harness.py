@@ -304,3 +304,29 @@ def test_bposd_reference_default_matches_oracle(gpu_available, oracle_lib, preci
     assert np.array_equal(res.corrections, ref)
     assert np.array_equal(res.fail, logical_failures(code.logicals.z, rd_h, ref))
     assert res.bp_converged < 3000  # OSD ran
+
+
+@pytest.mark.parametrize("bp_method", ["ms", "ps"])
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_bposd_hybrid_matches_oracle_loop(gpu_available, oracle_lib, bp_method, precision):
+    """bposd_hybrid end to end at R = 1 (BP-only on H_st 216x558, fold, corrected
+    readout re-syndromed on Hz, BP+OSD-CS on Hz): corrections and failure flags
+    == oracle/harness_py.hybrid_corrections, the loop-for-loop restatement of
+    BPOSDHybridCorrect.readout_correction
+    (/root/reference/python/qldpc/misc/_experiment.py:115-126)."""
+    from exp_ldpc_amd.experiment import BatchPipeline
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    from exp_ldpc_amd.storage_sim import build_storage_simulation
+    from oracle.harness_py import hybrid_corrections, logical_failures
+    code = load_code("hgp_12_3_4_s1234")
+    R, p = 1, 0.02
+    opts = {"max_iter": 40, "bp_method": bp_method, "ms_scaling_factor": 0, "osd_method": "osd_cs", "osd_order": 7}
+    priors = (2 * p / 3, 2 * p / 3)
+    pipe = BatchPipeline(code, R, "bposd_hybrid", opts, priors, precision=precision)
+    sim = build_storage_simulation(R, depolarizing_noise(p, p), code)
+    syn, rd = sim.sample_device(pipe.sampler_graph, 2000, seed=3, stream_id=11)
+    res = pipe.run(syn, rd, want_corrections=True)
+    syn_h, rd_h = syn.cpu().numpy(), rd.cpu().numpy()
+    ref = hybrid_corrections(oracle_lib, code.checks.z, R, syn_h, rd_h, opts, priors, precision=precision)
+    assert np.array_equal(res.corrections, ref)
+    assert np.array_equal(res.fail, logical_failures(code.logicals.z, rd_h, ref))

@@ -4,8 +4,13 @@ package's own code sources (exp_ldpc_amd/hgp.py, lifted.py):
 * C3  [[144,12,12]] bivariate-bicycle lift -> wave kernels, BP + SSF
 * C4  biregular_hgp(80,3,4,seed=2025), n = 10^4 (reference-generated fixture)
       -> workgroup kernels with HBM message scratch, BP + SSF
-* C5  PSL(2,q) matrix lift: q = 5 (n = 2700) and q = 13 (n = 49,140), BP on Hz
-      and on the R = 1 spacetime graph (multi-round syndromes)
+* C5  as BASELINE names it: the PSL(2,16) Cayley-graph lifted-product code
+      lifted_product_code_pgl2(1, 4, 2, double_cover=False, seed=1), n = 53,040,
+      k = 4080 (fixture tests/golden/lp_pgl2_1_4_2_s1_*): BP + SSF + logical check
+      at R = 0, and the R = 1 spacetime graph (48,960 x 130,560) with fold +
+      logical check, on the slot-group kernel (the default for graphs whose
+      messages spill to HBM) and on the workgroup kernel
+* extra graphs: PSL(2,q) matrix lifts, q = 5 (n = 2700) and q = 13 (n = 49,140)
 
 Every output is compared bit-for-bit with the CPU oracle on the same sampled
 storage-experiment shots (min-sum LLRs within the fp tolerance of
@@ -81,9 +86,10 @@ def test_hgp10k_bp_ssf_parity(gpu_available, oracle_lib, hgp10k):
     assert got["ssf_steps"].sum() > 0
 
 
-def test_hgp10k_lane_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
-    """The opt-in shot-lane HBM-streaming kernel (QDEC_LANE_KERNEL=1) on C4."""
-    monkeypatch.setenv("QDEC_LANE_KERNEL", "1")
+def test_hgp10k_group_kernel_forced_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
+    """The slot-group HBM-streaming kernel forced (QDEC_GROUP_KERNEL=1) on C4 in
+    fp32, where the LDS-resident kernel is the default."""
+    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1")
     hx, hz, lz = hgp10k
     p = 0.03
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=9, shot0=0, B=160)
@@ -132,14 +138,14 @@ def test_psl13_lift_bp_parity(gpu_available, oracle_lib, psl13_hz):
     _decode_both(oracle_lib, hz, 2 * p / 3, syn, max_iter=15)
 
 
-@pytest.mark.parametrize("kernel", ["workgroup", "lane"])
+@pytest.mark.parametrize("kernel", ["workgroup", "group"])
 def test_psl13_lift_spacetime_r1_parity(gpu_available, oracle_lib, psl13_hz, kernel, monkeypatch):
-    """C5's multi-round spacetime syndromes: H_st = [blockdiag(Hz, Hz) | M]
-    (spacetime_code.py:46-75), sampled by the storage-experiment sampler at R = 1
-    and folded onto the data qubits."""
+    """The PSL(2,13) matrix lift's multi-round spacetime syndromes: H_st =
+    [blockdiag(Hz, Hz) | M] (spacetime_code.py:46-75), sampled by the
+    storage-experiment sampler at R = 1 and folded onto the data qubits; both
+    HBM-message kernels."""
     from exp_ldpc_amd.spacetime import SpacetimeCode
-    if kernel == "lane":
-        monkeypatch.setenv("QDEC_LANE_KERNEL", "1")
+    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1" if kernel == "group" else "0")
     hz = psl13_hz
     H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
     p = 0.005
@@ -175,8 +181,10 @@ def test_hgp10k_lds_kernel_parity(gpu_available, oracle_lib, hgp10k, p):
 
 
 def test_hgp10k_workgroup_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
-    """The HBM-message workgroup kernel stays covered on C4 (QDEC_LDS_KERNEL=0)."""
+    """The HBM-message workgroup kernel stays covered on C4 (QDEC_LDS_KERNEL=0,
+    QDEC_GROUP_KERNEL=0)."""
     monkeypatch.setenv("QDEC_LDS_KERNEL", "0")
+    monkeypatch.setenv("QDEC_GROUP_KERNEL", "0")
     hx, hz, lz = hgp10k
     p = 0.03
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=12, shot0=0, B=96)
@@ -216,3 +224,90 @@ def test_hgp10k_ssf_rescan_kernel_parity(gpu_available, oracle_lib, hgp10k, monk
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=13, shot0=0, B=96)
     got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=30, keys=KEYS_SSF)
     assert got["ssf_steps"].sum() > 0
+
+
+# ------------------------------------------------------------------ config 5 as named
+@pytest.fixture(scope="module")
+def c5():
+    """BASELINE config 5: the PSL(2,16) Cayley-graph LP code (checks and
+    logicals from the committed fixture, tools/fixtures/make_c5_fixture.py)."""
+    from conftest import load_logicals
+    hx, hz = load_checks("lp_pgl2_1_4_2_s1")
+    _, lz = load_logicals("lp_pgl2_1_4_2_s1")
+    assert hz.shape == (24480, 53040) and lz.shape == (4080, 53040)
+    return hx, hz, lz
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("kernel", ["group", "workgroup"])
+def test_c5_r0_bp_ssf_fail_parity(gpu_available, oracle_lib, c5, precision, kernel, monkeypatch):
+    """Config 5 at R = 0: BP min-sum (max_iter 50) + SSF on the Hx flip sets +
+    logical check, 256 sampled shots, every output bit-exact."""
+    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1" if kernel == "group" else "0")
+    hx, hz, lz = c5
+    p = 0.004
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=21, shot0=0, B=256)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, precision=precision, keys=KEYS_SSF)
+    assert (got["status"] & 1).mean() < 1.0 and got["ssf_steps"].sum() > 0
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_c5_spacetime_r1_fold_fail_parity(gpu_available, oracle_lib, c5, precision):
+    """Config 5's multi-round spacetime syndromes: R = 1 (H_st 48,960 x 130,560,
+    spacetime_code.py:46-75), BP min-sum max_iter 50, corrections folded onto the
+    data qubits and the logical check, 256 shots, on the slot-group kernel."""
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    _, hz, lz = c5
+    H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
+    assert H.shape == (48960, 130560)
+    p = 0.002
+    syn, rd = oracle_lib.sample_storage(hz, 1, p, p, seed=SEED, stream=22, shot0=0, B=256)
+    got = _decode_both(oracle_lib, H, 2 * p / 3, syn, rd=rd, lz=lz, precision=precision,
+                       keys=("x", "corr", "iters", "status", "fail"), n_data=hz.shape[1], fold_blocks=2)
+    assert 0 < got["fail"].sum() < 256 or (got["status"] & 1).all()
+
+
+def test_c5_spacetime_r1_product_sum_f64(gpu_available, oracle_lib, c5):
+    """Product-sum (the reference CLI's default bp_method) in f64 on config 5's
+    R = 1 spacetime graph, slot-group kernel: x, folded corrections, iterations,
+    status and failure flags bit-exact."""
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+    _, hz, lz = c5
+    H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
+    p = 0.002
+    syn, rd = oracle_lib.sample_storage(hz, 1, p, p, seed=SEED, stream=23, shot0=0, B=128)
+    _decode_both(oracle_lib, H, 2 * p / 3, syn, rd=rd, lz=lz, method="ps", precision="f64", max_iter=30,
+                 keys=("x", "corr", "iters", "status", "fail"), n_data=hz.shape[1], fold_blocks=2)
+
+
+def test_group_kernel_llr_and_ragged(gpu_available, oracle_lib, monkeypatch):
+    """The slot-group kernel forced on a ragged random graph (check degrees 0..9,
+    column degrees 0..5, per-column priors): min-sum and product-sum, f32 and
+    f64, with more shots than slots so slots are refilled mid-flight; x,
+    iterations, status and LLRs (min-sum exact, product-sum within the device
+    log tolerance)."""
+    from test_gpu_parity import _cmp_llr
+    from exp_ldpc_amd.codes import make_check_matrix
+    from exp_ldpc_amd.decoder import Decoder
+    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1")
+    rng = np.random.default_rng(17)
+    m, n = 700, 1500
+    rows, colcount = [], np.zeros(n, int)
+    for i in range(m):
+        d = int(rng.integers(0, 10))
+        cand = [j for j in rng.permutation(n) if colcount[j] < 5][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    H = make_check_matrix(rows, n)
+    e = (rng.random((700, n)) < 0.03).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.uniform(0.01, 0.08, n)
+    for method in ("ms", "ps"):
+        for precision in ("f32", "f64"):
+            dec = Decoder(H, probs, method=method, precision=precision, max_iter=25)
+            got = dec.decode(syn, want=("x", "llr", "iters", "status"))
+            ref = oracle_lib.decode(H, probs, syn, method=method, precision=precision, max_iter=25)
+            for k in ("x", "iters", "status"):
+                assert np.array_equal(got[k], ref[k]), (method, precision, k)
+            _cmp_llr(got["llr"], ref["llr"], method, precision)

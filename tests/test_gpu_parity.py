@@ -420,3 +420,35 @@ def test_lds_kernel_ssf_fold(gpu_available, oracle_lib, code225, monkeypatch):
                             lz=lz, readout=rd, want_llr=False)
     for key in ("corr", "iters", "status", "fail"):
         assert np.array_equal(got[key], ref[key]), key
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision):
+    """The benchmarked instantiation (bp_ms_wave_kernel<.., LEAN=true, ..>, chosen
+    when x / corr / llr are all null) pinned bit-exactly: exactly bench.py's
+    decode_device call (syn + readout in; iters, status, ssf_steps, fail out) at
+    all 9 sweep points, 4096 device-sampled shots each (bench.py's sampler
+    streams, shot offset of its step 3), f64 headline and f32 variant, every
+    output compared with the oracle on the same shots."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    code = load_code("hgp_12_3_4_s1234")
+    hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
+    dev = torch.device("cuda", 0)
+    B, seed, shot0 = 4096, 20250221, 3 * (1 << 18)
+    for pi, p in enumerate(np.geomspace(1e-3, 1e-1, 9)):
+        dec = Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0,
+                      flip_sets=hx, logicals=lz)
+        syn = torch.empty((B, hz.shape[0]), dtype=torch.uint8, device=dev)
+        rd = torch.empty((B, hz.shape[1]), dtype=torch.uint8, device=dev)
+        dec.sample_storage_device(0, p, p, seed, pi, shot0, B, syn, rd)
+        out = {k: torch.empty(B, dtype=dt, device=dev) for k, dt in
+               (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
+        dec.decode_device(B, syn=syn, readout=rd, **out)
+        torch.cuda.synchronize()
+        rs, rr = oracle_lib.sample_storage(hz, 0, p, p, seed=seed, stream=pi, shot0=shot0, B=B)
+        assert np.array_equal(syn.cpu().numpy(), rs) and np.array_equal(rd.cpu().numpy(), rr), p
+        ref = oracle_lib.decode(hz, 2 * p / 3, rs, method="ms", precision=precision, max_iter=50, ssf=True, gens=hx,
+                                lz=lz, readout=rr, want_llr=False, ssf_impl="fast")
+        for k in out:
+            assert np.array_equal(out[k].cpu().numpy(), ref[k]), (p, k)

@@ -154,3 +154,34 @@ def test_psl2_13_lift_size():
     hx, hz = code.checks.x, code.checks.z
     prod = (hx.astype(np.int64) @ hz.T.astype(np.int64)).tocsr()
     assert not np.any(prod.data % 2)
+
+
+def test_config5_pgl2_16_cayley_lp_fixture():
+    """BASELINE config 5 as named: lifted_product_code_pgl2(1, 4, 2,
+    double_cover=False, seed=1) over PGL(2,16) = PSL(2,16) (|G| = 4080, 3
+    Morgenstern generators, reference lifted_product_code.py:411-453).  The
+    construction reproduces the committed fixture, n = (2w)^2/4 + r^2 times |G|
+    (the size bound of the reference's own test_lifted_product_code.py), and the
+    committed logicals satisfy the CSS relations (Hx Lz^T = 0, Hz Lx^T = 0,
+    Lx Lz^T = I) with k = 4080."""
+    import scipy.sparse as sp
+    from conftest import load_checks, load_logicals
+    gens = L.morgenstern_generators(1, 4)
+    assert len(gens) == 3 and len(L.dfs_generators(gens[0].identity(), gens)) == 4080
+    code = L.lifted_product_code_pgl2(1, 4, 2, compute_logicals=False, seed=1, double_cover=False)
+    hx, hz = load_checks("lp_pgl2_1_4_2_s1")
+    assert code.num_qubits == ((2 * 3) ** 2 // 4 + 2 ** 2) * 4080 == 53040
+    for got, ref in ((code.checks.x, hx), (code.checks.z, hz)):
+        got = sp.csr_matrix(got)
+        assert got.shape == ref.shape and (got != ref).nnz == 0
+    assert not ((hz @ hx.T).toarray() % 2).any()
+    lx, lz = load_logicals("lp_pgl2_1_4_2_s1")
+    assert lz.shape == lx.shape == (4080, 53040)
+    assert not ((hx @ lz.T).toarray() % 2).any() and not ((hz @ lx.T).toarray() % 2).any()
+    pair = sp.csr_matrix(lx.astype(np.int64) @ lz.T.astype(np.int64))
+    pair.data %= 2
+    pair.eliminate_zeros()
+    assert (pair != sp.identity(4080, dtype=np.int64, format="csr")).nnz == 0
+    # the default double_cover wrapper raises the reference's block-length error
+    with pytest.raises(ValueError):
+        L.lifted_product_code_pgl2(1, 4, 2, compute_logicals=False, seed=1)

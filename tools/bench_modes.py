@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--bp_method", default="ps")
     ap.add_argument("--max_iter", type=int, default=225)
     ap.add_argument("--host-osd", action="store_true", help="also time the host OSD stage")
+    ap.add_argument("--precision", default="f64", choices=["f32", "f64"],
+                    help="BP message precision (default f64, as ldpc v1 and the harness default)")
     a = ap.parse_args()
     code = load_code("hgp_12_3_4_s1234")
     ps = a.p or [0.003, 0.01, 0.03]
@@ -47,7 +49,8 @@ def main():
         for p in ps:
             noise = depolarizing_noise(p, p)
             sim = build_storage_simulation(rounds, noise, code)
-            pipe = BatchPipeline(code, rounds, mode, opts, (2 * p / 3, 2 * p / 3), noise=noise)
+            pipe = BatchPipeline(code, rounds, mode, opts, (2 * p / 3, 2 * p / 3), noise=noise,
+                                 precision=a.precision)
             batches = [sim.sample_device(pipe.sampler_graph, a.batch, 20250221, 0, s) for s in
                        range(0, a.shots, a.batch)]
             variants = [("device_osd", None)]
@@ -72,6 +75,7 @@ def main():
                     Decoder.osd_device_supported = orig
                 n = a.batch * len(batches)
                 print(json.dumps({"mode": mode, "rounds": rounds, "p": p, "variant": vname, "bp_method": a.bp_method,
+                                  "precision": a.precision,
                                   "max_iter": a.max_iter, "shots": n, "shots_per_s": n / dt, "ler": fails / n,
                                   "bp_converged_frac": conv / n}), flush=True)
 
