@@ -545,11 +545,16 @@ void build_tables(qd_graph* G, int m, int n) {
     }
     std::vector<int32_t> edge_csc(std::max(E, 1), 0);
     for (int e = 0; e < E; ++e) edge_csc[e] = G->col_ptr[ci[e]] + edge_cpos[e];
+    // edge arrays padded by kEdgePad zeros (unguarded whole-row index loads)
+    col_edge.resize((size_t)E + kEdgePad, 0);
+    edge_csc.resize((size_t)E + kEdgePad, 0);
+    std::vector<int32_t> ci_pad(G->col_idx);
+    ci_pad.resize((size_t)E + kEdgePad, 0);
     g.col_ptr = G->arena.upload(G->col_ptr);
     g.col_edge = G->arena.upload(col_edge);
     g.edge_csc = G->arena.upload(edge_csc);
     g.row_ptr = G->arena.upload(G->row_ptr);
-    g.col_idx = G->arena.upload(G->col_idx);
+    g.col_idx = G->arena.upload(ci_pad);
     int rc = 0, rv = 0, drc = 0;
     g.wave = (g.max_rdeg <= kDR && g.max_cdeg <= kDC && pick_wave_shape(m, n, g.max_rdeg, &rc, &rv, &drc)) ? 1 : 0;
     if (!g.wave) {  // workgroup kernels: plain 64-padding, no wave tables
@@ -618,8 +623,6 @@ void build_tables(qd_graph* G, int m, int n) {
         g.slots[p].r_cslot = G->arena.upload(r_cslot[p]);
         g.slots[p].c_rslot = G->arena.upload(c_rslot[p]);
     }
-    g.row_ptr = G->arena.upload(G->row_ptr);
-    g.col_idx = G->arena.upload(G->col_idx);
     ms_layout(G, m, n, edge_cpos);
 }
 
@@ -1015,6 +1018,19 @@ int qd_graph_set_priors(qd_graph* G, const double* probs) {
         }
         g.prior[QD_PRODUCT_SUM][QD_F64] = G->prior_arena.upload(ps64);
         g.prior[QD_PRODUCT_SUM][QD_F32] = G->prior_arena.upload(ps32);
+        {  // by CSR edge, padded (slot-group kernel)
+            const size_t ne = (size_t)g.E + kEdgePad;
+            std::vector<double> ems64(ne, 0.0), eps64(ne, 0.0);
+            std::vector<float> ems32(ne, 0.0f), eps32(ne, 0.0f);
+            for (int e = 0; e < g.E; ++e) {
+                const int j = G->col_idx[e];
+                ems64[e] = ms64[j], eps64[e] = ps64[j], ems32[e] = ms32[j], eps32[e] = ps32[j];
+            }
+            g.eprior[QD_MIN_SUM][QD_F64] = G->prior_arena.upload(ems64);
+            g.eprior[QD_MIN_SUM][QD_F32] = G->prior_arena.upload(ems32);
+            g.eprior[QD_PRODUCT_SUM][QD_F64] = G->prior_arena.upload(eps64);
+            g.eprior[QD_PRODUCT_SUM][QD_F32] = G->prior_arena.upload(eps32);
+        }
         G->has_priors = true;
     });
 }

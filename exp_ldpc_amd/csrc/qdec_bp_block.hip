@@ -654,7 +654,7 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
 //   xw  [n]  u64    hard decision of column j for every slot (one ballot)
 //   pw  [m]  u64    parity of check i under the hard decision (residual words)
 //   rw  [n_data] u64  residual readout ^ corr of slots being finalised
-// Per iteration: check pass (waves split the checks, kGrpU checks per step with
+// Per iteration: check pass (waves split the checks, UC checks per step with
 // all their loads issued first), barrier, column pass (waves split the
 // columns), barrier, syndrome test (lanes split the checks: each lane xors the
 // 64-slot hard-decision words of its row, so one pass tests all 64 slots),
@@ -675,7 +675,26 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
 // message model (fp32; 32*E fp64) plus O(m + n) bytes of words.
 constexpr int kGrpWaves = 8;
 constexpr int kGrpThreads = 64 * kGrpWaves;
-constexpr int kGrpU = 4;              // checks / columns per wave step (loads in flight)
+// Checks / columns per wave step: every load of a step is issued before any is
+// used, so a wave keeps UC * DR (check pass) or UV * (column degree) loads of
+// whole 64-slot lines in flight; the column pass has few edges per column, so
+// it takes more columns per step.  (QDEC_GRP_UC / QDEC_GRP_UV: A/B defines.)
+template <typename T, int DR>
+constexpr int grp_uc() {
+#ifdef QDEC_GRP_UC
+    return QDEC_GRP_UC;
+#else
+    return sizeof(T) == 4 ? 4 : (DR <= 8 ? 4 : 2);
+#endif
+}
+template <typename T, int DC>
+constexpr int grp_uv() {
+#ifdef QDEC_GRP_UV
+    return QDEC_GRP_UV;
+#else
+    return sizeof(T) == 4 ? (DC <= 4 ? 16 : 8) : (DC <= 4 ? 8 : 4);
+#endif
+}
 constexpr int kFinPerCu = 8;          // SSF/finalize workgroups per CU when their state is in HBM
 constexpr size_t kGrpHeader = 256;    // scratch header: the shot counter
 
@@ -688,8 +707,8 @@ __host__ __device__ inline size_t grp_round(size_t b) { return (b + 255) / 256 *
 __host__ __device__ inline GroupLayout group_layout(const DevGraph& g, size_t tsz) {
     GroupLayout L;
     L.v2c = 0;
-    L.c2v = L.v2c + grp_round((size_t)g.E * 64 * tsz);
-    L.sw = L.c2v + grp_round((size_t)g.E * 64 * tsz);
+    L.c2v = L.v2c + grp_round(((size_t)g.E + kEdgePad) * 64 * tsz);
+    L.sw = L.c2v + grp_round(((size_t)g.E + kEdgePad) * 64 * tsz);
     L.xw = L.sw + grp_round((size_t)g.m * 8);
     L.pw = L.xw + grp_round((size_t)g.n * 8);
     L.rw = L.pw + grp_round((size_t)g.m * 8);
@@ -711,7 +730,8 @@ __global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, Decod
                                                                const int32_t* __restrict__ cp,
                                                                const int32_t* __restrict__ ce,
                                                                const int32_t* __restrict__ ecs,
-                                                               const T* __restrict__ prior) {
+                                                               const T* __restrict__ prior,
+                                                               const T* __restrict__ ep) {
     __shared__ unsigned long long s_bad, s_fail;
     __shared__ long long s_base;
     __shared__ int s_qbase;
@@ -765,84 +785,96 @@ __global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, Decod
         const bool fresh = it == 1;  // first pass of this slot's shot: v2c = priors
         // Every lane runs the passes, idle slots on garbage, so control flow is
         // wave-uniform: scalar branches, no exec masking.
-        for (int i0 = wv * kGrpU; i0 < m; i0 += kGrpWaves * kGrpU) {  // check pass
-            int e0[kGrpU], d[kGrpU], par[kGrpU];
-            T v[kGrpU][DR];
+        constexpr int UC = grp_uc<T, DR>(), UV = grp_uv<T, DC>();
+        // Loads first, for the whole step (scalar-guarded by the row / column
+        // degree, 32-bit offsets), then the arithmetic with pad positions masked
+        // by selects (Big for the row minimum, the neutral factor 1 for the
+        // products), so no load waits behind another's use.
+        for (int i0 = wv * UC; i0 < m; i0 += kGrpWaves * UC) {  // check pass
+            int e0[UC], d[UC], par[UC];
+            T mv[UC][DR], pv[UC][DR];
 #pragma unroll
-            for (int u = 0; u < kGrpU; ++u) {
+            for (int u = 0; u < UC; ++u) {
                 const int i = i0 + u;
-                e0[u] = i < m ? rp[i] : 0;
-                d[u] = i < m ? rp[i + 1] - e0[u] : 0;
-                // sw is written by this kernel: a volatile (vector) load, never the scalar cache
-                par[u] = i < m ? (int)((*(volatile const uint64_t*)&sw[i] >> lane) & 1ull) : 0;
+                const int ii = i < m ? i : m - 1;
+                e0[u] = rp[ii];
+                d[u] = i < m ? rp[ii + 1] - e0[u] : 0;
             }
 #pragma unroll
-            for (int u = 0; u < kGrpU; ++u)
+            for (int u = 0; u < UC; ++u)
 #pragma unroll
                 for (int t = 0; t < DR; ++t)
-                    if (t < d[u]) {
-                        const T mv = v2c[(size_t)(e0[u] + t) * 64];
-                        const T pv = prior[ci[e0[u] + t]];
-                        v[u][t] = fresh ? pv : mv;
-                    }
+                    if (t < d[u]) mv[u][t] = v2c[(uint32_t)(e0[u] + t) * 64u];
 #pragma unroll
-            for (int u = 0; u < kGrpU; ++u) {
+            for (int u = 0; u < UC; ++u) {
+                const int ii = i0 + u < m ? i0 + u : m - 1;
+                // sw is written by this kernel: a volatile (vector) load, never the scalar cache
+                par[u] = (int)((*(volatile const uint64_t*)&sw[ii] >> lane) & 1ull);
+#pragma unroll
+                for (int t = 0; t < DR; ++t) pv[u][t] = ep[e0[u] + t];  // padded array: unguarded
+            }
+#pragma unroll
+            for (int u = 0; u < UC; ++u) {
+                T v[DR];
+#pragma unroll
+                for (int t = 0; t < DR; ++t) v[t] = fresh ? pv[u][t] : mv[u][t];
                 if constexpr (METHOD == 1) {
                     T m1 = Big<T>::v, m2 = Big<T>::v;
                     int pu = par[u];
 #pragma unroll
-                    for (int t = 0; t < DR; ++t)
-                        if (t < d[u]) {
-                            const T av = fabs(v[u][t]);
-                            m2 = med3(av, m1, m2);
-                            m1 = fmin(m1, av);
-                            pu ^= v[u][t] <= (T)0;
-                        }
+                    for (int t = 0; t < DR; ++t) {
+                        const bool on = t < d[u];
+                        const T av = on ? fabs(v[t]) : Big<T>::v;  // Big changes neither minimum
+                        m2 = med3(av, m1, m2);
+                        m1 = fmin(m1, av);
+                        pu ^= on && v[t] <= (T)0;
+                    }
                     const T m1a = m1 * alpha, m2a = m2 * alpha;
 #pragma unroll
                     for (int t = 0; t < DR; ++t)
                         if (t < d[u]) {
-                            const T y = (fabs(v[u][t]) == m1) ? m2a : m1a;
-                            c2v[(size_t)ecs[e0[u] + t] * 64] = (pu ^ (v[u][t] <= (T)0)) ? -y : y;
+                            const T y = (fabs(v[t]) == m1) ? m2a : m1a;
+                            c2v[(uint32_t)ecs[e0[u] + t] * 64u] = (pu ^ (v[t] <= (T)0)) ? -y : y;
                         }
                 } else {
                     T r[DR], fw[DR];
                     T f = par[u] ? (T)-1 : (T)1;
 #pragma unroll
-                    for (int t = 0; t < DR; ++t)
-                        if (t < d[u]) {
-                            fw[t] = f;
-                            r[t] = (T)2 / ((T)1 + v[u][t]) - (T)1;
-                            f *= r[t];
-                        }
+                    for (int t = 0; t < DR; ++t) {
+                        fw[t] = f;
+                        r[t] = t < d[u] ? (T)2 / ((T)1 + v[t]) - (T)1 : (T)1;  // pads: the neutral factor
+                        f *= r[t];
+                    }
                     T b = (T)1;
 #pragma unroll
-                    for (int t = DR - 1; t >= 0; --t)
+                    for (int t = DR - 1; t >= 0; --t) {
                         if (t < d[u]) {
                             const T c = fw[t] * b;
-                            c2v[(size_t)ecs[e0[u] + t] * 64] = ((T)1 - c) / ((T)1 + c);
-                            b *= r[t];
+                            c2v[(uint32_t)ecs[e0[u] + t] * 64u] = ((T)1 - c) / ((T)1 + c);
                         }
+                        b *= r[t];
+                    }
                 }
             }
         }
         __syncthreads();
-        for (int j0 = wv * kGrpU; j0 < n; j0 += kGrpWaves * kGrpU) {  // column pass
-            int t0[kGrpU], d[kGrpU];
-            T c[kGrpU][DC];
+        for (int j0 = wv * UV; j0 < n; j0 += kGrpWaves * UV) {  // column pass
+            int t0[UV], d[UV];
+            T c[UV][DC];
 #pragma unroll
-            for (int u = 0; u < kGrpU; ++u) {
+            for (int u = 0; u < UV; ++u) {
                 const int j = j0 + u;
-                t0[u] = j < n ? cp[j] : 0;
-                d[u] = j < n ? cp[j + 1] - t0[u] : 0;
+                const int jj = j < n ? j : n - 1;
+                t0[u] = cp[jj];
+                d[u] = j < n ? cp[jj + 1] - t0[u] : 0;
             }
 #pragma unroll
-            for (int u = 0; u < kGrpU; ++u)
+            for (int u = 0; u < UV; ++u)
 #pragma unroll
                 for (int t = 0; t < DC; ++t)
-                    if (t < d[u]) c[u][t] = c2v[(size_t)(t0[u] + t) * 64];  // CSC order: contiguous
+                    if (t < d[u]) c[u][t] = c2v[(uint32_t)(t0[u] + t) * 64u];  // CSC order: contiguous
 #pragma unroll
-            for (int u = 0; u < kGrpU; ++u) {
+            for (int u = 0; u < UV; ++u) {
                 const int j = j0 + u;
                 if (j >= n) break;
                 T pre[DC];
@@ -850,20 +882,19 @@ __global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, Decod
                 bool hard;
                 if constexpr (METHOD == 1) {
 #pragma unroll
-                    for (int t = 0; t < DC; ++t)
-                        if (t < d[u]) {
-                            pre[t] = acc;
-                            acc += c[u][t];
-                        }
+                    for (int t = 0; t < DC; ++t) {
+                        pre[t] = acc;
+                        acc = t < d[u] ? acc + c[u][t] : acc;
+                    }
                     hard = acc <= (T)0;
                 } else {
 #pragma unroll
-                    for (int t = 0; t < DC; ++t)
-                        if (t < d[u]) {
-                            pre[t] = acc;
-                            acc *= c[u][t];
-                            if (isnan(acc)) acc = (T)1;
-                        }
+                    for (int t = 0; t < DC; ++t) {
+                        pre[t] = acc;
+                        T x = acc * c[u][t];
+                        if (isnan(x)) x = (T)1;
+                        acc = t < d[u] ? x : acc;
+                    }
                     hard = acc >= (T)1;
                 }
                 const uint64_t hw = __ballot(hard);
@@ -878,7 +909,7 @@ __global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, Decod
 #pragma unroll
                     for (int t = DC - 1; t >= 0; --t)
                         if (t < d[u]) {
-                            v2c[(size_t)ce[t0[u] + t] * 64] = pre[t] + suf;
+                            v2c[(uint32_t)ce[t0[u] + t] * 64u] = pre[t] + suf;
                             suf += c[u][t];
                         }
                 } else {
@@ -886,7 +917,7 @@ __global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, Decod
 #pragma unroll
                     for (int t = DC - 1; t >= 0; --t)
                         if (t < d[u]) {
-                            v2c[(size_t)ce[t0[u] + t] * 64] = pre[t] * suf;
+                            v2c[(uint32_t)ce[t0[u] + t] * 64u] = pre[t] * suf;
                             suf *= c[u][t];
                             if (isnan(suf)) suf = (T)1;
                         }
@@ -1316,11 +1347,15 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
     int cap = 0;
     T* gs = nullptr;
     DecodeArgs a = a0;
+    // placement 0 with SSF: the SSF/finalize workgroups keep their shot state in
+    // HBM too, in the scratch tail (kFinPerCu workgroups per CU)
+    const bool fin_hbm = a0.ssf && placement == 0;
+    const size_t fin_bytes = fin_hbm ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
     if (placement != 3) {
         // scratch = header (dynamic shot counter) + per-workgroup slices in HBM
         const size_t per_wg = block_slice_bytes(g, sizeof(T), placement);
-        if (!scratch || per_wg == 0 || scratch_bytes <= kGrpHeader) return (int)hipErrorInvalidValue;
-        const long long max_wg = (long long)((scratch_bytes - kGrpHeader) / per_wg);
+        if (!scratch || per_wg == 0 || scratch_bytes <= kGrpHeader + fin_bytes) return (int)hipErrorInvalidValue;
+        const long long max_wg = (long long)((scratch_bytes - kGrpHeader - fin_bytes) / per_wg);
         // the grid is num_cus * cap workgroups, each owning one slice: at least
         // one slice per CU (block_scratch_bytes sizes 4 per CU)
         if (max_wg < num_cus) return (int)hipErrorOutOfMemory;
@@ -1356,13 +1391,14 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
     hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
     if (e != hipSuccess) return (int)e;
     record_ev(a, 0, stream);
-    if (!(placement & 2)) return (int)hipErrorNotSupported;  // SSF keeps its shot state in LDS
     int rc = unr ? launch_block(bp_block_kernel<T, METHOD, true, UR, UC>, lds, a.B, num_cus, stream, cap, g, a, gs,
                                 placement)
                  : launch_block(bp_block_kernel<T, METHOD, true>, lds, a.B, num_cus, stream, cap, g, a, gs, placement);
     record_ev(a, 1, stream);
     if (rc != 0) return rc;
-    rc = launch_ssf_fin(g, a, num_cus, stream);
+    rc = fin_hbm ? launch_block2(ssf_block_kernel, kCtrl, a.B, num_cus, stream, g, a,
+                                 static_cast<unsigned char*>(scratch) + (scratch_bytes - fin_bytes), kFinPerCu)
+                 : launch_ssf_fin(g, a, num_cus, stream);
     record_ev(a, 2, stream);
     return rc;
 }
@@ -1480,7 +1516,8 @@ static int launch_group_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     record_ev(a, 0, stream);
     hipLaunchKernelGGL((bp_group_kernel<T, METHOD, DR, DC>), dim3((unsigned)grid), dim3(kGrpThreads), 0, stream, g, a,
                        base, gb, g.row_ptr, g.col_idx, g.col_ptr, g.col_edge, g.edge_csc,
-                       reinterpret_cast<const T*>(g.prior[METHOD][sizeof(T) == 4 ? 1 : 0]));
+                       reinterpret_cast<const T*>(g.prior[METHOD][sizeof(T) == 4 ? 1 : 0]),
+                       reinterpret_cast<const T*>(g.eprior[METHOD][sizeof(T) == 4 ? 1 : 0]));
     const hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;
@@ -1513,8 +1550,10 @@ size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num
     }
     const int placement = block_placement(g, tsz);
     if (placement == 3) return 0;
-    // shot-counter header + up to 4 workgroup slices per CU
-    return kGrpHeader + (size_t)num_cus * 4 * block_slice_bytes(g, tsz, placement);
+    // shot-counter header + up to 4 workgroup slices per CU (+ the SSF/finalize
+    // shot state when it lives in HBM)
+    const size_t fin = (a.ssf && placement == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
+    return kGrpHeader + (size_t)num_cus * 4 * block_slice_bytes(g, tsz, placement) + fin;
 }
 
 int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,

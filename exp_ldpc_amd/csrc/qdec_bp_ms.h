@@ -322,8 +322,20 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
         uint64_t X[RV];
         bool pres[RC];
         int it = 1;
-        bool conv = false;
-        for (; it <= a.max_iter; ++it) {
+#ifdef QDEC_CALIB_NOBP
+        // HBM calibration variant (tools/dev/gpu_calib.sh): the same staging,
+        // queue and output traffic with the BP loop compiled out; every shot
+        // "converges" at once with the zero hard decision
+        constexpr bool kSkipBp = true;
+#pragma unroll
+        for (int rv = 0; rv < RV; ++rv) X[rv] = 0ull;
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) pres[rc] = sbit[rc];
+#else
+        constexpr bool kSkipBp = false;
+#endif
+        bool conv = kSkipBp;
+        for (; !kSkipBp && it <= a.max_iter; ++it) {
             const T alpha = alpha_bits<T>(it, a.ms_scaling);
             // ---- check pass: state (m1, m2) with the parity in both signs ----
 #pragma unroll

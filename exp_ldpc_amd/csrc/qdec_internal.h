@@ -14,6 +14,7 @@ constexpr int kMlDC = 4;         // LDS-resident min-sum kernel: max variable de
 constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
 constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
 constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
+constexpr int kEdgePad = 16;     // index / prior arrays padded past E (>= the largest row / column width)
 
 // Wave-kernel shapes (check rounds RC, variable rounds RV, check-node compute
 // width D <= kDR): a graph is padded to the first shape that holds it (RC*64 >= m,
@@ -58,12 +59,17 @@ struct DevGraph {
     const uint8_t* c_deg;         // [n_pad]
     SlotTables slots[2];          // [QD_F64], [QD_F32]
     const void* prior[2][2];      // [method][precision] initial message per column, [n_pad]
+    // the same by CSR edge (the prior of edge e's column), [E + kEdgePad]
+    // (slot-group kernel: one load per edge, no column-index chain)
+    const void* eprior[2][2];
     // CSR / CSC copies (sampler; workgroup kernels)
     const int32_t* row_ptr;
     const int32_t* col_idx;
     const int32_t* col_ptr;       // [n+1]
     const int32_t* col_edge;      // [E] CSR edge ids of column j, ascending row
     const int32_t* edge_csc;      // [E] CSC position (col_ptr[col] + rank in column) of CSR edge e
+    // col_idx, col_edge and edge_csc carry kEdgePad zero entries past E, so a
+    // kernel may load a whole row's (column's) worth of indices unguarded
     // min-sum wave kernel with compressed check state (qdec_bp_ms.h).  Variables
     // sit in lane slots sorted by degree (ms_vslot); slot edge k scatters its v2c
     // message to element (etab & 0xffff) and gathers check state (etab >> 16);

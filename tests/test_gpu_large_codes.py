@@ -97,6 +97,18 @@ def test_hgp10k_group_kernel_forced_parity(gpu_available, oracle_lib, hgp10k, mo
     assert got["ssf_steps"].sum() > 0
 
 
+@pytest.mark.parametrize("p", [0.01, 0.03])
+def test_hgp10k_f64_bp_ssf_fail_parity(gpu_available, oracle_lib, hgp10k, p):
+    """C4 at ldpc's precision: BP min-sum f64 max_iter 50 (the slot-group kernel,
+    messages in HBM) + SSF + logical check, 256 sampled shots, bit-exact."""
+    hx, hz, lz = hgp10k
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=14, shot0=0, B=256)
+    got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=50, precision="f64",
+                       keys=KEYS_SSF)
+    if p >= 0.03:
+        assert (got["status"] & 1).mean() < 0.9 and got["ssf_steps"].sum() > 0
+
+
 def test_hgp10k_bp_f64_llr(gpu_available, oracle_lib, hgp10k):
     from test_gpu_parity import _cmp_llr
     from exp_ldpc_amd.decoder import Decoder
