@@ -25,7 +25,10 @@ Phases (rank 0 prints ONE JSON line):
      events the library records on the launch stream around each kernel; the
      roofline uses these (overlapped launches share the chip, so their durations
      are not one kernel's);
-  4. sampling + decode: K steps with the sampler inside the timed region.
+  4. sampling + decode: K steps with the sampler inside the timed region;
+  5. (rank 0, N = 1) `large_code_roofline`: the HBM-bound path, BASELINE config 5
+     (n = 53,040 Cayley-graph LP code, R = 1 spacetime syndromes) on the
+     slot-group kernel, one timed launch with its HBM roofline fraction.
 
 Multi-GPU: `torchrun --nproc-per-node N bench.py --gpus N` (one process per
 GPU), or `python bench.py --gpus N`, which starts that torchrun as a child
@@ -159,6 +162,68 @@ def cpu_baseline(code, ps, args):
                             "sample": f"{per32} shots per point (shot indices 0..{per32 - 1}), BP min-sum f32, "
                                       f"otherwise as the f64 leg; {e32:.1f} s of CPU work",
                             "failures_per_point": f32, "shots_per_point": per32}]
+    return res
+
+
+def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
+    """HBM roofline of the genuinely HBM-bound path: BASELINE config 5 (PSL(2,16)
+    Cayley-graph LP code, n = 53,040) at R = 1 spacetime syndromes (H_st
+    48,960 x 130,560, E = 236,640), BP min-sum f64 max_iter 50 + fold + logical
+    check on the slot-group kernel, whose messages stream through HBM.  One
+    warmup launch, one timed launch (HIP events around the BP kernel on its
+    launch stream).  Algorithmic bytes = 32 B per edge per shot-iteration (f64
+    v2c read + c2v write in the check pass, c2v read + v2c write in the column
+    pass) + the per-shot I/O (syndrome, readout, outputs)."""
+    import scipy.sparse as sp
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    from exp_ldpc_amd.spacetime import SpacetimeCode
+
+    def csr(path, key):  # committed fixture (tools/fixtures/make_c5_fixture.py)
+        d = np.load(os.path.join(REPO, "tests", "golden", path))
+        return sp.csr_matrix((np.ones(d[key + "_indices"].size, np.uint8), d[key + "_indices"], d[key + "_indptr"]),
+                             shape=tuple(d[key + "_shape"]))
+    hz = csr("lp_pgl2_1_4_2_s1_checks.npz", "hz")
+    lz = csr("lp_pgl2_1_4_2_s1_logicals.npz", "lz")
+    H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
+    m, n = H.shape
+    nd = hz.shape[1]
+    sampler = Decoder(hz, 2 * p / 3, method="ms", precision="f64", max_iter=50, device=dev.index)
+    dec = Decoder(H, 2 * p / 3, method="ms", precision="f64", max_iter=50, logicals=lz, n_data=nd, fold_blocks=2,
+                  device=dev.index)
+    syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
+    rd = torch.empty((2, shots, nd), dtype=torch.uint8, device=dev)
+    for b in range(2):
+        sampler.sample_storage_device(1, p, p, SEED, 100, b * shots, shots, syn[b], rd[b])
+    iters = torch.empty((2, shots), dtype=torch.int32, device=dev)
+    status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+    fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+    dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
+    torch.cuda.synchronize(dev)
+    dec.set_timing(1)
+    t0 = time.perf_counter()
+    dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1])
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    bp_ms, _ = dec.read_timing()
+    it_sum = int(iters[1].to(torch.int64).sum().item())
+    E = int(H.nnz)
+    io = shots * (m + nd + 1 + 1 + 4)
+    algo = 32 * E * it_sum + io
+    achieved = algo / (float(bp_ms[0]) * 1e-3) / 1e9
+    res = {"config": "C5 as named: PSL(2,16) Cayley-graph LP (lifted_product_code_pgl2(1,4,2,double_cover=False,"
+                     "seed=1)), n=53040 k=4080, R=1 spacetime 48960x130560 E=236640, BP min-sum f64 max_iter 50, "
+                     f"fold + logical check, p={p}, {shots} device-sampled shots per launch",
+           "kernel": "qdec::bp_group_kernel<double, 1, 8, 4> (slot groups, messages in HBM)",
+           "shots_per_s": shots / wall, "bp_kernel_ms": float(bp_ms[0]), "mean_bp_iters": it_sum / shots,
+           "ler": float(fail[1].to(torch.float64).mean().item()),
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "algorithmic_bytes_per_launch": algo,
+                        "bytes_model": "32 B per edge per shot-iteration (f64 messages: v2c read + c2v write, c2v "
+                                       "read + v2c write) + per-shot I/O"}}
+    del syn, rd, dec, sampler
+    torch.cuda.empty_cache()
     return res
 
 
@@ -331,6 +396,8 @@ def main():
                          "--streams streams")
     ap.add_argument("--iso-steps", type=int, default=2, help="isolated (one-stream) steps timing each kernel")
     ap.add_argument("--no-sample-phase", action="store_true", help="skip the sampling+decode phase")
+    ap.add_argument("--no-large-code", action="store_true",
+                    help="skip the config-5 HBM-roofline line (large_code_roofline; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     args.iso_steps = max(1, min(args.iso_steps, args.steps))
@@ -416,6 +483,10 @@ def main():
         sd_elapsed = run.timed(decs, args.steps, run.streams[:1], sampler=decs[0], warm=False)
         sd = total_shots / sd_elapsed
 
+    large = None
+    if rank == 0 and world == 1 and not fake and not args.no_large_code:
+        large = large_code_roofline(dev)
+
     if rank == 0:
         value = total_shots / elapsed
         cpu = None
@@ -473,6 +544,23 @@ def main():
                                 **{key: dv.get(key) for key in ("valu_issue_frac", "lds_frac",
                                                                 "lds_bank_conflict_ratio", "hbm_frac", "clock_ghz",
                                                                 "duration_ms", "formulas")}}
+            # the binding on-chip ceiling: HBM is `bound` by the §8(d) contract,
+            # but the kernel's messages never leave LDS / registers, so what
+            # limits it is the busier of the LDS array and the VALU issue
+            lf, vf = dv.get("lds_frac"), dv.get("valu_issue_frac")
+            if lf is not None and vf is not None:
+                roof["on_chip_bound"] = {
+                    "unit": "lds" if lf >= vf else "valu", "lds_busy": lf, "valu_issue": vf,
+                    "lds_bank_conflict_ratio": dv.get("lds_bank_conflict_ratio"),
+                    "note": "per-wave LDS traffic per BP iteration (f64): 8 row reads, 2 state writes, "
+                            "14 state gathers, 14 v2c scatters (DESIGN.md §4); HBM frac above is compulsory I/O"}
+        calib = os.path.join(REPO, "profiles", "r03_hbm_calibration")
+        if os.path.isdir(calib):
+            roof["traffic_calibration"] = {
+                "source": os.path.relpath(calib, REPO),
+                "note": "FETCH_SIZE of this kernel equals that of a staging-only build with the BP loop compiled "
+                        "out (QDEC_CALIB_NOBP): the messages add no HBM bytes; traffic above the compulsory I/O is "
+                        "the LDS-DMA row staging (whole 256-B dword blocks per row) and 1-4 B scattered outputs"}
 
         result = {
             "metric": METRIC, "value": value, "unit": "shots/s", "n_gpus": world, "steps": args.steps,
@@ -498,6 +586,8 @@ def main():
             result["sample_and_decode"] = {"value": sd, "unit": "shots/s", "dtype": args.precision, "streams": 1,
                                            "note": "on-device sampling inside the timed region, one stream"}
         result["roofline"] = roof
+        if large is not None:
+            result["large_code_roofline"] = large
         if cpu is not None:
             result["cpu_baseline"] = cpu
         result["ler"] = ler

@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
 // ---------------------------------------------------------------- slot-group BP
 // BP for graphs whose messages do not fit LDS (configs 4 and 5: 10^4 to 1.3*10^5
 // columns), laid out so every HBM access of the message loops is a whole
-// cache line.  A workgroup of kGrpWaves waves decodes a group of 64 shot slots
+// cache line.  A workgroup of grp_waves<T>() waves decodes a group of 64 shot slots
 // together: lane l of every wave works on slot l.  The group owns a scratch
 // block in HBM:
 //   v2c [E][64] T   messages by CSR edge, slot-minor: a wave reading edge e of
@@ -673,8 +673,19 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
 // product-sum: ldpc's forward/backward products and NaN guards), with alpha_t
 // of the slot's own iteration.  HBM traffic per shot-iteration: the 16*E-byte
 // message model (fp32; 32*E fp64) plus O(m + n) bytes of words.
-constexpr int kGrpWaves = 8;
-constexpr int kGrpThreads = 64 * kGrpWaves;
+// Waves per group: 4 for f32 (a 4-wave group fits 3 waves per SIMD, i.e. three
+// groups per CU: +30 % on config 5 against 8-wave groups), 8 for f64 (register
+// bound at 2 waves per SIMD either way; 8-wave groups finish and refill slots
+// with twice the threads: config 4 f64 at p = 0.005, 2.9 iterations per shot,
+// 604 k vs 401 k shots/s).  QDEC_GRP_WAVES overrides both (A/B define).
+template <typename T>
+constexpr int grp_waves() {
+#ifdef QDEC_GRP_WAVES
+    return QDEC_GRP_WAVES;
+#else
+    return sizeof(T) == 4 ? 4 : 8;
+#endif
+}
 // Checks / columns per wave step: every load of a step is issued before any is
 // used, so a wave keeps UC * DR (check pass) or UV * (column degree) loads of
 // whole 64-slot lines in flight; the column pass has few edges per column, so
@@ -723,7 +734,7 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 }
 
 template <typename T, int METHOD, int DR, int DC>
-__global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, DecodeArgs a, unsigned char* scratch,
+__global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph g, DecodeArgs a, unsigned char* scratch,
                                                                size_t group_bytes,
                                                                const int32_t* __restrict__ rp,
                                                                const int32_t* __restrict__ ci,
@@ -732,6 +743,7 @@ __global__ __launch_bounds__(kGrpThreads) void bp_group_kernel(DevGraph g, Decod
                                                                const int32_t* __restrict__ ecs,
                                                                const T* __restrict__ prior,
                                                                const T* __restrict__ ep) {
+    constexpr int kGrpWaves = grp_waves<T>(), kGrpThreads = 64 * kGrpWaves;
     __shared__ unsigned long long s_bad, s_fail;
     __shared__ long long s_base;
     __shared__ int s_qbase;
@@ -1457,17 +1469,18 @@ static int launch_lds(const DevGraph& g, const DecodeArgs& a, int num_cus, hipSt
 // ---------------------------------------------------------------- slot-group launch
 static size_t group_scratch_budget() {
     const char* v = getenv("QDEC_GROUP_SCRATCH_MB");
-    const long long mb = v ? atoll(v) : 65536;  // 64 GiB of the 288 GB HBM
+    const long long mb = v ? atoll(v) : 98304;  // 96 GiB of the 288 GB HBM
     return (size_t)std::max(64ll, mb) << 20;
 }
 
-// Groups in flight: up to 2 per CU (the kernel's occupancy), capped by the
-// scratch budget and by the batch (every slot should see >= 4 shots, so the
+// Groups in flight: as many per CU as the occupancy allows, capped by the
+// scratch budget and by the batch (every slot should see >= 2 shots, so the
 // tail of a launch stays short and small test batches stay small).
 static int64_t group_count(const DevGraph& g, size_t tsz, int num_cus, int64_t B) {
     const size_t per = group_layout(g, tsz).total;
-    int64_t c = std::min<int64_t>((int64_t)num_cus * 2, (int64_t)(group_scratch_budget() / per));
-    c = std::min<int64_t>(c, (B + 255) / 256);
+    const int waves = tsz == 4 ? grp_waves<float>() : grp_waves<double>();
+    int64_t c = std::min<int64_t>((int64_t)num_cus * (32 / waves), (int64_t)(group_scratch_budget() / per));
+    c = std::min<int64_t>(c, (B + 127) / 128);
     return std::max<int64_t>(c, 1);
 }
 
@@ -1499,6 +1512,7 @@ static int launch_group_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     unsigned char* fin_state = fin_hbm ? base + (scratch_bytes - fin_bytes) : nullptr;
     const int64_t max_groups = (int64_t)((scratch_bytes - fin_bytes - kGrpHeader) / gb);
     int per_cu = 0;
+    constexpr int kGrpThreads = 64 * grp_waves<T>();
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_group_kernel<T, METHOD, DR, DC>,
                                                                 kGrpThreads, 0);
     if (e != hipSuccess) return (int)e;

@@ -342,7 +342,8 @@ __device__ inline void finalize_shot(const DevGraph& g, const DecodeArgs& a, int
 // the dword-aligned address at or below the row start; `shift` is the row's
 // byte offset inside the staged bytes.  The readout is double buffered (shot s
 // reads its buffer at the end while s+1's lands).  Every stage issues the same
-// number of loads (past the batch end it re-reads shot 0; lanes past the buffer
+// number of loads (lanes past the row re-read its last dword, so a stage
+// fetches the row's lines only; past the batch end it re-reads shot 0; lanes past the buffer
 // read its last whole dword), so consumers wait with a counted vmcnt: vector
 // memory operations retire in issue order and the kStaged most recent ones are
 // the next shot's.  The final 1-3 bytes of a buffer whose length is not a
@@ -399,7 +400,13 @@ struct ShotIo {
         const int64_t start = row * len;
         const int64_t dw0 = start >> 2;
         const uint8_t* base = buf + 4 * dw0;
-        const int64_t lim64 = total_dw - 1 - dw0;  // last loadable dword, relative (>= 0)
+        int64_t lim64 = total_dw - 1 - dw0;  // last loadable dword, relative (>= 0)
+#ifndef QDEC_STAGE_BUFFER_CLAMP
+        // lanes past the row re-read the row's last dword (same line, coalesced
+        // in the instruction) instead of fetching the following rows' bytes
+        const int64_t row_last = ((start + len - 1) >> 2) - dw0;
+        lim64 = row_last < lim64 ? row_last : lim64;
+#endif
         const int lim = lim64 > 0x3fffffff ? 0x3fffffff : (int)lim64;
 #pragma unroll
         for (int c = 0; c < N; ++c) {
