@@ -222,6 +222,13 @@ def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
                         "algorithmic_bytes_per_launch": algo,
                         "bytes_model": "32 B per edge per shot-iteration (f64 messages: v2c read + c2v write, c2v "
                                        "read + v2c write) + per-shot I/O"}}
+    pmc = pmc_ceilings("qdec::bp_group_kernel<double, 1, 8, 4>")
+    if pmc is not None:  # committed PMC passes of the same launch shape (tools/gpu/r03f.sh)
+        src, name, k = pmc
+        dv = k["derived"]
+        res["roofline"]["traffic"] = dv.get("hbm_bytes_per_dispatch")
+        res["roofline"]["traffic_source"] = {"source": src, "kernel": name, "duration_ms": dv.get("duration_ms"),
+                                             "note": "2*FETCH_SIZE + WRITE_SIZE per dispatch, same config/shots"}
     del syn, rd, dec, sampler
     torch.cuda.empty_cache()
     return res
