@@ -81,19 +81,27 @@ class QuantumCodeChecks:
 
 @dataclass(frozen=True)
 class QuantumCodeLogicals:
-    """Dense logical operators, one per row (qecc_util.py:53-91)."""
+    """Logical operators, one per row (qecc_util.py:53-91): dense arrays as in
+    the reference, or scipy sparse matrices (an extension for codes with
+    thousands of sparse logicals, e.g. config 5's k = 4080 of weight 3, whose
+    dense form is 866 MB; stored as a private CSR copy)."""
     x: np.ndarray
     z: np.ndarray
 
     def __post_init__(self):
+        for name in ("x", "z"):
+            a = getattr(self, name)
+            if sp.issparse(a):
+                object.__setattr__(self, name, sp.csr_matrix(a, copy=True))
         _require_integral(self.x)
         _require_integral(self.z)
         if self.x.shape[1] != self.z.shape[1]:
             raise ValueError("x and z logicals act on an inconsistent number of qubits")
         if self.x.shape[0] != self.z.shape[0]:
             raise ValueError("Number of provided X and Z logical operators mismatch")
-        self.x.flags.writeable = False
-        self.z.flags.writeable = False
+        for a in (self.x, self.z):
+            if not sp.issparse(a):
+                a.flags.writeable = False
 
     @property
     def num_qubits(self) -> int:

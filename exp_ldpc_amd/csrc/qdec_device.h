@@ -90,6 +90,23 @@ __device__ __forceinline__ void lds_load(const T* p, T (&v)[D]) {
     }
 }
 
+// The first N elements of a 16-B aligned row: 16-byte loads, then one 8-byte
+// load for an odd f64 tail (a degree-7 f64 row: 3 x ds_read_b128 + ds_read_b64,
+// 14 LDS cycles instead of the 16 of four b128 loads).  Elements >= N of v are
+// left unset.
+template <typename T, int N, int D>
+__device__ __forceinline__ void lds_load_first(const T* p, T (&v)[D]) {
+    static_assert(N <= D && sizeof(T) == 8, "f64 rows");
+    using V = __attribute__((ext_vector_type(2))) T;
+#pragma unroll
+    for (int c = 0; c < N / 2; ++c) {
+        V x = *reinterpret_cast<const V*>(p + 2 * c);
+        v[2 * c] = x[0];
+        v[2 * c + 1] = x[1];
+    }
+    if constexpr (N % 2) v[N - 1] = p[N - 1];
+}
+
 __device__ __forceinline__ long long wave_max_i64(long long v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {

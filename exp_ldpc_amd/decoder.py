@@ -119,7 +119,7 @@ class Decoder:
         failure check; handed over as CSR supports (qd_graph_set_logicals_csr),
         so codes with thousands of sparse logicals never build a dense k x n
         array."""
-        L = sp.csr_matrix(lz if sp.issparse(lz) else np.asarray(lz) % 2)
+        L = sp.csr_matrix(lz, copy=True) if sp.issparse(lz) else sp.csr_matrix(np.asarray(lz) % 2)
         if L.ndim != 2 or L.shape[1] != self.n_data:
             raise ValueError("logicals must be k x n_data")
         L.sum_duplicates()

@@ -86,7 +86,7 @@ class BatchPipeline:
         L = code.logicals.x if use_x_logicals else code.logicals.z
         self.H = sp.csr_matrix(H)
         self.m, self.n = self.H.shape
-        self.L = np.asarray(L) % 2
+        self.L = sp.csr_matrix(L) if sp.issparse(L) else np.asarray(L) % 2
         o = bp_osd_options
         common = dict(method=o.get("bp_method", "ps"), precision=precision, max_iter=int(o.get("max_iter", 0) or 0),
                       ms_scaling=float(o.get("ms_scaling_factor", 0.0)), device=self.device)
@@ -141,7 +141,7 @@ class BatchPipeline:
     def _fail_host(self, readout, corr):
         if self.L.shape[0] == 0:
             return np.zeros(readout.shape[0], bool)
-        return ((((readout ^ corr).astype(np.int64)) @ self.L.T.astype(np.int64)) % 2).any(axis=1)
+        return ((np.asarray(((readout ^ corr).astype(np.int64)) @ self.L.T.astype(np.int64))) % 2).any(axis=1)
 
     def _osd_fix(self, dec, osd, syn_d, status_d, llr_d, B):
         """OSD for shots whose BP did not converge; returns (idx, osdw) on host."""

@@ -5,6 +5,7 @@ harness argument handling mirrors the reference."""
 import argparse
 
 import numpy as np
+import scipy.sparse as sp
 import pytest
 
 from conftest import load_checks
@@ -176,3 +177,21 @@ def test_checkpoint_append_keeps_file_parseable(tmp_path):
     assert _load_checkpoint(ck) == {}
     _append_checkpoint_row(ck, {"p_ph": 0.05, "failures": 1, "samples": 100, "precision": "f64", "config_fp": "gh"})
     assert set(_load_checkpoint(ck)) == {(0.05, "gh")}
+
+
+def test_sparse_logicals_accepted_and_copied():
+    """QuantumCodeLogicals keeps scipy-sparse logicals as a private CSR copy
+    (config 5's k = 4080 never goes dense); dense inputs stay read-only."""
+    from exp_ldpc_amd.codes import QuantumCodeLogicals
+    lz = sp.random(6, 40, density=0.1, format="coo", random_state=1, dtype=np.float64)
+    lz.data[:] = 1
+    lz = lz.astype(np.uint8)
+    q = QuantumCodeLogicals(lz.tocsc(), lz)
+    assert sp.isspmatrix_csr(q.x) and q.num_logicals == 6 and q.num_qubits == 40
+    assert np.array_equal(q.z.toarray(), lz.toarray())
+    q.z.data[:] = 0                     # the caller's matrix is untouched
+    assert lz.toarray().any()
+    with pytest.raises(TypeError):
+        QuantumCodeLogicals(lz.astype(np.float32), lz)
+    d = QuantumCodeLogicals(lz.toarray(), lz.toarray())
+    assert not d.x.flags.writeable

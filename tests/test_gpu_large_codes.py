@@ -323,3 +323,30 @@ def test_group_kernel_llr_and_ragged(gpu_available, oracle_lib, monkeypatch):
             for k in ("x", "iters", "status"):
                 assert np.array_equal(got[k], ref[k]), (method, precision, k)
             _cmp_llr(got["llr"], ref["llr"], method, precision)
+            # fewer shots than one group's 64 slots (idle slots from the start)
+            small = dec.decode(syn[:5], want=("x", "iters", "status"))
+            for k in ("x", "iters", "status"):
+                assert np.array_equal(small[k], ref[k][:5]), (method, precision, "B=5", k)
+
+
+def test_c5_run_simulation_bpssf_matches_oracle(gpu_available, oracle_lib, c5):
+    """The harness end to end on config 5 (reference run_simulation with
+    BPSSFCorrect, R = 0): the code carries its 4080 logicals as sparse CSR
+    (codes.QuantumCodeLogicals), shots come from the device sampler, and the
+    per-shot failure flags equal the CPU oracle's on the same Philox shots."""
+    from exp_ldpc_amd.codes import QuantumCode, QuantumCodeChecks, QuantumCodeLogicals
+    from exp_ldpc_amd.experiment import run_simulation
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    from conftest import load_logicals
+    hx, hz, lz = c5
+    lx, _ = load_logicals("lp_pgl2_1_4_2_s1")
+    code = QuantumCode(QuantumCodeChecks(hx, hz), QuantumCodeLogicals(lx, lz))
+    opts = {"max_iter": 50, "bp_method": "ms", "ms_scaling_factor": 0, "osd_method": "osd0", "osd_order": 0}
+    p = 0.004
+    pr = 2 * p / 3
+    fails = run_simulation(256, code, lambda a, b: pr, lambda a, b: pr, depolarizing_noise, {"p": p, "pm": p}, opts,
+                           0, "bpssf", seed=3, batch=256, precision="f64")
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=3, stream=0, shot0=0, B=256)
+    ref = oracle_lib.decode(hz, pr, syn, method="ms", precision="f64", max_iter=50, ssf=True, gens=hx, lz=lz,
+                            readout=rd, want_llr=False, ssf_impl="fast")
+    assert np.array_equal(fails, ref["fail"].astype(bool))
