@@ -212,7 +212,11 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
         // groups of 32, class = dword % 32, cost max(4, L0 + L1).  f64
         // (ds_write_b64): 4 groups of 16 contiguous lanes, class = element % 16,
         // cost max(6, sum of L).  Row positions are free (min/sign over the row).
-        const int ngl = p == 1 ? 2 : 4, ncl = p == 1 ? 32 : 16, floor_c = p == 1 ? 4 : 6;
+        // f64: the transfer of a ds_write_b64 takes 6 cycles but every array
+        // cycle beyond 4 is a bank-conflict cycle the CU's other waves wait
+        // for (PMC: the array is the busiest unit), so the floor is 4
+        static const bool v1 = std::getenv("QDEC_MS_LAYOUT_V1") != nullptr;  // A/B: round-2 layout
+        const int ngl = p == 1 ? 2 : 4, ncl = p == 1 ? 32 : 16, floor_c = p == 1 ? 4 : (v1 ? 6 : 4);
         const int lanes_per = 64 / ngl;
         std::vector<int> grp(E), lg(E), pos(E);
         for (int i = 0; i < m; ++i)
@@ -288,8 +292,13 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
         // hardware's grouping, class = slot % 16).  Only distinct slots in one
         // class of one group conflict; the anneal below minimises the sum over
         // instructions and groups of the worst class load.
-        std::vector<int> sst(m);
-        for (int i = 0; i < m; ++i) sst[i] = i;
+        // every check lane, pads included, writes its state once per iteration:
+        // f64 ds_write_b128 (8 groups of 8 contiguous lanes, class = slot % 8),
+        // f32 ds_write_b64 (4 groups of 16, class = slot % 16); the anneal adds
+        // the worst class load of each group (round 2 placed only the gathers:
+        // modelled 37 state-write array cycles per iteration for f64, ideal 16)
+        std::vector<int> sst(g.m_pad);
+        for (int i = 0; i < g.m_pad; ++i) sst[i] = i;
         {
             const int rcl = p == 1 ? 32 : 16;
             auto rgroup = [&](int l) -> int {
@@ -327,40 +336,59 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
                 if (gpad[q]) mx = std::max(mx, ++cnt[g.m_pad % rcl]);
                 return mx;
             };
-            std::vector<int> qc(NGR);
+            const int wl = p == 1 ? 16 : 8;  // state-write group width = classes
+            const int NW = v1 ? 0 : g.m_pad / wl;
+            auto wcost = [&](int w) {
+                int cnt[16] = {0};
+                int mx = 0;
+                for (int t = 0; t < wl; ++t) mx = std::max(mx, ++cnt[sst[w * wl + t] % wl]);
+                return mx;
+            };
+            std::vector<int> qc(NGR), wc(NW);
             long cur = 0;
             for (int q = 0; q < NGR; ++q) cur += (qc[q] = qcost(q));
+            for (int w = 0; w < NW; ++w) cur += (wc[w] = wcost(w));
             std::vector<int> occ(g.m_pad, -1);
-            for (int i = 0; i < m; ++i) occ[sst[i]] = i;
+            for (int i = 0; i < g.m_pad; ++i) occ[sst[i]] = i;
             std::vector<int> best = sst;
             long bestc = cur;
             const int iters = 60000;
             std::vector<int> aff;
             std::vector<int> newc;
+            // v1 moves real checks only (pads take the free slots afterwards)
+            const int nmov = v1 ? m : g.m_pad;
             for (int it = 0; it < iters; ++it) {
                 const double T = 0.6 * (1.0 - (double)it / iters) + 0.02;
-                const int c1 = (int)(rng() % (unsigned)m);
+                const int c1 = (int)(rng() % (unsigned)nmov);
                 const int s2 = (int)(rng() % (unsigned)g.m_pad);
                 const int c2 = occ[s2];
                 if (c2 == c1) continue;
-                aff = app[c1];
-                if (c2 >= 0) aff.insert(aff.end(), app[c2].begin(), app[c2].end());
+                aff = app[c1 < m ? c1 : 0];
+                if (c1 >= m) aff.clear();
+                if (c2 >= 0 && c2 < m) aff.insert(aff.end(), app[c2].begin(), app[c2].end());
                 std::sort(aff.begin(), aff.end());
                 aff.erase(std::unique(aff.begin(), aff.end()), aff.end());
+                const int w1 = NW ? c1 / wl : -1, w2 = NW && c2 >= 0 && c2 / wl != w1 ? c2 / wl : -1;
                 long old = 0;
                 for (int q : aff) old += qc[q];
+                if (w1 >= 0) old += wc[w1];
+                if (w2 >= 0) old += wc[w2];
                 const int s1 = sst[c1];
                 sst[c1] = s2;
                 if (c2 >= 0) sst[c2] = s1;
                 newc.resize(aff.size());
                 long nw = 0;
                 for (size_t t = 0; t < aff.size(); ++t) nw += (newc[t] = qcost(aff[t]));
+                const int nw1 = w1 >= 0 ? wcost(w1) : 0, nw2 = w2 >= 0 ? wcost(w2) : 0;
+                nw += nw1 + nw2;
                 const long d = nw - old;
                 const double u = (double)(rng() & 0xFFFFFF) / 16777216.0;
                 if (d <= 0 || u < std::exp(-(double)d / T)) {
                     occ[s2] = c1;
                     occ[s1] = c2;
                     for (size_t t = 0; t < aff.size(); ++t) qc[aff[t]] = newc[t];
+                    if (w1 >= 0) wc[w1] = nw1;
+                    if (w2 >= 0) wc[w2] = nw2;
                     cur += d;
                     if (cur < bestc) { bestc = cur; best = sst; }
                 } else {
@@ -371,8 +399,11 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
             sst = best;
         }
         std::vector<uint16_t> ss16(g.m_pad, (uint16_t)g.m_pad);
-        {   // pad check lanes write the zero state's slot with zeros (min-sum of
-            // an empty row never reaches it: their rows hold Big); keep them apart
+        if (!v1) {
+            // pad check lanes write zeros into their own slots (min-sum of an
+            // empty row never reaches them: their rows hold Big)
+            for (int i = 0; i < g.m_pad; ++i) ss16[i] = (uint16_t)sst[i];
+        } else {
             for (int i = 0; i < m; ++i) ss16[i] = (uint16_t)sst[i];
             std::vector<char> used(g.m_pad + 1, 0);
             for (int i = 0; i < m; ++i) used[sst[i]] = 1;
