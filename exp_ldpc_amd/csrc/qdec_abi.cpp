@@ -149,7 +149,6 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
     const int E = rp[m];
     const int drc = g.shape_drc;
     const int RVn = g.n_pad / 64;
-    const int DRSf = drs<float>();
     // Lane slots of the variables: ascending column degree (stable), so the
     // leading 64-variable rounds whose variables all have degree <= 3 run a
     // 3-edge variable pass (ms_d3r).  Each variable's arithmetic is unchanged.
@@ -1046,6 +1045,13 @@ int qd_graph_set_priors(qd_graph* G, const double* probs) {
             }
             g.ms_prior[QD_F64] = G->prior_arena.upload(s64);
             g.ms_prior[QD_F32] = G->prior_arena.upload(s32);
+            // all priors > 0: the wave kernel's zero-syndrome shortcut applies
+            bool pos64 = true, pos32 = true;
+            for (int j = 0; j < g.n; ++j) {
+                pos64 = pos64 && ms64[j] > 0.0;
+                pos32 = pos32 && ms32[j] > 0.0f;
+            }
+            g.ms_allpos = (pos64 ? 1 << QD_F64 : 0) | (pos32 ? 1 << QD_F32 : 0);
         }
         g.prior[QD_PRODUCT_SUM][QD_F64] = G->prior_arena.upload(ps64);
         g.prior[QD_PRODUCT_SUM][QD_F32] = G->prior_arena.upload(ps32);

@@ -240,6 +240,11 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
     int sslot[RC];  // where this lane's checks write their state (host-placed)
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc) sslot[rc] = g.ms_sslot[PREC][rc * 64 + lane];
+    // zero syndrome + every prior > 0: iteration 1 converges with x = 0 (all
+    // messages are >= 0, so every posterior is >= its prior > 0), and the LEAN
+    // outputs (iterations 1, converged, failure from the readout alone) need
+    // nothing else
+    const bool zero_ok = LEAN && ((g.ms_allpos >> PREC) & 1);
     uint64_t smask[RC][RV];
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc)
@@ -304,17 +309,27 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
             }
         }
 
-        // ---- initial messages: v2c = prior ----
+        // ---- initial messages: v2c = prior (held in registers as vp and
+        // written to the rows unless the shot is skipped) ----
         V2 vp[NP][kDC];  // v2c messages this lane sent last iteration, round pairs
 #pragma unroll
         for (int p = 0; p < NP; ++p)
 #pragma unroll
             for (int k = 0; k < kDC; ++k) vp[p][k] = L[p];
+        bool skip = false;
+        if (zero_ok) {
+            bool any = false;
 #pragma unroll
-        for (int rv = 0; rv < RV; ++rv)
+            for (int rc = 0; rc < RC; ++rc) any |= sbit[rc];
+            skip = __ballot(any) == 0ull;
+        }
+        if (!skip) {
 #pragma unroll
-            for (int k = 0; k < kDC; ++k)
-                if (!(rv < D3P && k == 3)) v2c[etab[rv][k] & 0xffff] = (rv % 2 == 0) ? L[rv / 2].x : L[rv / 2].y;
+            for (int rv = 0; rv < RV; ++rv)
+#pragma unroll
+                for (int k = 0; k < kDC; ++k)
+                    if (!(rv < D3P && k == 3)) v2c[etab[rv][k] & 0xffff] = (rv % 2 == 0) ? L[rv / 2].x : L[rv / 2].y;
+        }
         wave_lds_sync();
 
         QDEC_STAMP(1);
@@ -335,7 +350,14 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
         constexpr bool kSkipBp = false;
 #endif
         bool conv = kSkipBp;
-        for (; !kSkipBp && it <= a.max_iter; ++it) {
+        if (skip) {
+            conv = true;
+#pragma unroll
+            for (int rv = 0; rv < RV; ++rv) X[rv] = 0ull;
+#pragma unroll
+            for (int rc = 0; rc < RC; ++rc) pres[rc] = false;
+        }
+        for (; !kSkipBp && !skip && it <= a.max_iter; ++it) {
             const T alpha = alpha_bits<T>(it, a.ms_scaling);
             // ---- check pass: state (m1, m2) with the parity in both signs ----
 #pragma unroll
