@@ -15,7 +15,9 @@ f32 (the stated-tolerance variant) and reported under `variants`.
 Phases (rank 0 prints ONE JSON line):
   1. headline: W warmup + K timed steps, the 9 points round-robin over --streams
      HIP streams (default 9: every point on its own stream; measured 79 vs 76 M
-     f64 shots/s at 5), so kernels of independent points fill each other's tails
+     f64 shots/s at 5), so kernels of independent points fill each other's tails;
+     f64 wave kernels run at 12 waves per CU here (--wave-occupancy; a lone
+     decode keeps 8, its own optimum)
      (--schedule pipeline: every BP kernel on one stream and every SSF kernel on
      a second one behind an event -- measured slower: the persistent BP kernel
      fills every CU, so SSF only runs in BP's tail, which it cannot fill because
@@ -256,6 +258,9 @@ class FakeDecoder:
     def set_timing(self, capacity):
         self.cap = capacity
 
+    def set_wave_occupancy(self, waves_per_cu=0):
+        pass
+
     def read_timing(self):
         return np.full(self.cap, 1e-3), np.full(self.cap, 1e-3)
 
@@ -401,6 +406,9 @@ def main():
                     help="pipeline: every BP kernel on one stream, every SSF kernel on a second one behind an "
                          "event (point i's SSF overlaps point i+1's BP); streams: points round-robin over "
                          "--streams streams")
+    ap.add_argument("--wave-occupancy", type=int, default=-1,
+                    help="waves per CU of the wave BP kernels in the overlapped phases (qd_graph_set_wave_occupancy); "
+                         "-1 = 12 for f64 when the points share the chip over several streams, else the default")
     ap.add_argument("--iso-steps", type=int, default=2, help="isolated (one-stream) steps timing each kernel")
     ap.add_argument("--no-sample-phase", action="store_true", help="skip the sampling+decode phase")
     ap.add_argument("--no-large-code", action="store_true",
@@ -451,7 +459,22 @@ def main():
         run.sample(decs[0], s)
     run.sync()
 
+    def occupancy(precision):
+        """Waves per CU for the overlapped phases: concurrent points (several
+        streams) run f64 at full occupancy, 12 waves per CU (82-83 vs 80 M
+        shots/s at 8, profiles/r03_ab_layout/occupancy_streams_sweep.json); a
+        lone decode keeps the default (8: faster alone)."""
+        if args.wave_occupancy >= 0:
+            return args.wave_occupancy
+        return 12 if precision == "f64" and args.schedule == "streams" and len(run.streams) > 1 else 0
+
+    def set_occupancy(dset, w):
+        for d in dset:
+            d.set_wave_occupancy(w)
+
     # ---- phase 1: headline precision, overlapped (pipeline or streams) ----
+    occ = {args.precision: occupancy(args.precision)}
+    set_occupancy(decs, occ[args.precision])
     run.pipelined(decs, True)
     elapsed = run.timed(decs, args.steps, run.streams)
     run.pipelined(decs, False)
@@ -463,6 +486,8 @@ def main():
     variant = None
     if args.variant not in ("none", args.precision):
         vdecs = decoders(args.variant)
+        occ[args.variant] = occupancy(args.variant)
+        set_occupancy(vdecs, occ[args.variant])
         run.pipelined(vdecs, True)
         v_elapsed = run.timed(vdecs, args.steps, run.streams)
         run.pipelined(vdecs, False)
@@ -472,6 +497,7 @@ def main():
     # ---- phase 3: isolated launches (one stream) for per-kernel durations ----
     iso = {}
     for prec, dset in [(args.precision, decs)] + ([(variant[0], variant[4])] if variant else []):
+        set_occupancy(dset, 0)  # one stream: the lone-decode default
         for d in dset:
             d.set_timing(args.iso_steps)
         run.timed(dset, args.iso_steps, run.streams[:1], warm=False)  # every launch is timed
@@ -580,7 +606,8 @@ def main():
                                    "alpha_t=1-2^-t + SSF (Hx flip sets) + fused logical check",
                        "shots_per_point_per_step_per_gpu": args.batch, "global_batch": args.batch * P * world,
                        "parallelism": f"shot-sharded x{world}, no collective",
-                       "schedule": args.schedule if args.schedule == "pipeline" else f"{args.streams} streams"},
+                       "schedule": args.schedule if args.schedule == "pipeline" else f"{args.streams} streams",
+                       "wave_waves_per_cu": {k: (v or "default") for k, v in occ.items()}},
         }
         if variant:
             vb, vs, _ = iso[variant[0]]

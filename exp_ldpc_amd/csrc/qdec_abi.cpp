@@ -1241,6 +1241,14 @@ int qd_graph_set_ssf_stream(qd_graph* G, void* ssf_stream) {
     });
 }
 
+int qd_graph_set_wave_occupancy(qd_graph* G, int32_t waves_per_cu) {
+    return guarded([&] {
+        check_graph(G);
+        if (waves_per_cu < 0 || waves_per_cu > 64) throw Fail(-62, "waves_per_cu outside [0, 64]");
+        G->dg.wave_occ = waves_per_cu;
+    });
+}
+
 int qd_graph_set_timing(qd_graph* G, int32_t capacity) {
     return guarded([&] {
         check_graph(G);

@@ -679,13 +679,10 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         }
         const bool lean = !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1 &&
                           (!DEFER || a.q_packed);
-        // f64: 2 waves per SIMD measured faster than 3 at every p (n = 225: 8.5 vs
-        // 10.3 ms per 2^18 shots at p = 0.1, 0.51 vs 0.66 at p = 0.001)
-        static const int f64_cap = [] {  // diagnostics: QDEC_F64_WAVES_PER_CU replaces the f64 cap
-            const char* v = std::getenv("QDEC_F64_WAVES_PER_CU");
-            return v ? std::atoi(v) : 8;
-        }();
-        const int cap = sizeof(T) == 8 ? f64_cap : 0;
+        // f64: 2 waves per SIMD measured faster than 3 for a lone decode at every
+        // p (n = 225: 7.1 vs 9.3 ms per 2^18 shots at p = 0.1); concurrent
+        // decodes may ask for more (qd_graph_set_wave_occupancy)
+        const int cap = g.wave_occ > 0 ? g.wave_occ : (sizeof(T) == 8 ? 8 : 0);
         // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
             if (g.ms_d3r >= 2) {

@@ -84,6 +84,7 @@ struct DevGraph {
     const void* ms_prior[2];      // [precision][n_pad] min-sum priors in slot order
     int ms_d3r;                   // leading 64-slot rounds whose variables all have degree <= 3
     int ms_allpos;                // bit p: every prior LLR of precision p is > 0
+    int wave_occ;                 // qd_graph_set_wave_occupancy (0: default)
     // LDS-resident min-sum workgroup kernel (qdec_bp_block.hip, bp_ms_lds_kernel):
     // [kMlDC][n] LDS element of edge k of column j (row * kMlDRS + CSR position),
     // pad 0xffff; nullptr when the graph's degrees exceed kMlDRS / kMlDC

@@ -249,6 +249,13 @@ class Decoder:
             _abi.ptr(status), _abi.ptr(base), _abi.ptr(readout), _abi.ptr(osd0), _abi.ptr(osdw), _abi.ptr(corr),
             _abi.ptr(fail), C.c_void_p(stream)), "qd_osd_batch_device")
 
+    def set_wave_occupancy(self, waves_per_cu: int = 0) -> None:
+        """Waves per CU of the wave BP kernels (qd_graph_set_wave_occupancy):
+        0 = the default; more for decodes that run concurrently on several
+        streams.  Results do not depend on it."""
+        _abi.check(self._lib.qd_graph_set_wave_occupancy(self._handle, int(waves_per_cu)),
+                   "qd_graph_set_wave_occupancy")
+
     def set_ssf_stream(self, stream) -> None:
         """Run the SSF kernel of later decode_device calls on `stream` (a torch
         stream or a raw hipStream_t; None = the decode's own stream); see

@@ -178,6 +178,16 @@ int qd_graph_set_timing(qd_graph* g, int32_t capacity);
  * overlap is only possible between decodes on different handles.  Replaces
  * nothing in the reference (its decode is one synchronous call per shot). */
 int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
+
+/* Occupancy of the wave BP kernels (one wave per shot, persistent grid) in waves
+ * per CU: 0 = the default (f64: 8, measured fastest for a lone decode; f32: the
+ * hardware maximum), N > 0 = N, bounded by what the kernel's LDS and registers
+ * allow and rounded down to a multiple of 4 (equal waves per SIMD).  For
+ * several decodes running concurrently on different streams: the bench's
+ * 9-stream sweep measured 82-83 M shots/s at 12 f64 waves per CU against 80 M
+ * at 8, while a lone f64 decode at 12 is slower (p = 0.1: 9.3 vs 7.1 ms per 2^18
+ * shots).  Results are identical at every setting.  No reference counterpart. */
+int qd_graph_set_wave_occupancy(qd_graph* g, int32_t waves_per_cu);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
 
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out

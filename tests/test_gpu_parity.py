@@ -452,3 +452,65 @@ def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision):
                                 lz=lz, readout=rr, want_llr=False, ssf_impl="fast")
         for k in out:
             assert np.array_equal(out[k].cpu().numpy(), ref[k]), (p, k)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_lean_zero_syndrome_shortcut_and_nonpositive_priors(gpu_available, oracle_lib, precision):
+    """The LEAN kernel writes iteration 1 / converged / x = 0 directly for an
+    all-zero syndrome only when every prior LLR is > 0.  Per-column priors with
+    some p >= 0.5 (LLR <= 0: BP must run and need not converge at once) and the
+    same shots with all p < 0.5, a quarter of them zero syndromes: iterations,
+    status, SSF steps and failure flags equal the oracle's in both cases."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    code = load_code("hgp_12_3_4_s1234")
+    hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
+    rng = np.random.default_rng(11)
+    B, n = 2048, hz.shape[1]
+    e = (rng.random((B, n)) < 0.01).astype(np.uint8)
+    e[: B // 4] = 0
+    syn = np.ascontiguousarray(((hz @ e.T).T % 2).astype(np.uint8))
+    rd = (e ^ (rng.random((B, n)) < 0.002)).astype(np.uint8)
+    dev = torch.device("cuda", 0)
+    for probs in (rng.uniform(0.005, 0.02, n), np.where(np.arange(n) % 37 == 0, 0.6, 0.01)):
+        dec = Decoder(hz, probs, method="ms", precision=precision, max_iter=30, flip_sets=hx, logicals=lz)
+        out = {k: torch.empty(B, dtype=dt, device=dev) for k, dt in
+               (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
+        dec.decode_device(B, syn=torch.from_numpy(syn).to(dev), readout=torch.from_numpy(rd).to(dev), **out)
+        torch.cuda.synchronize()
+        ref = oracle_lib.decode(hz, probs, syn, method="ms", precision=precision, max_iter=30, ssf=True, gens=hx,
+                                lz=lz, readout=rd, want_llr=False, ssf_impl="fast")
+        for k in out:
+            assert np.array_equal(out[k].cpu().numpy(), ref[k]), (probs.max(), k)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_wave_occupancy_does_not_change_results(gpu_available, oracle_lib, precision):
+    """qd_graph_set_wave_occupancy (bench.py's overlapped phases use 12 f64
+    waves per CU) only changes the persistent grid: iterations, status, SSF
+    steps and failure flags equal the oracle's at 4, 12 and the default; an
+    out-of-range value is refused."""
+    import torch
+    from exp_ldpc_amd._abi import QdecError
+    from exp_ldpc_amd.decoder import Decoder
+    code = load_code("hgp_12_3_4_s1234")
+    hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
+    p, B = 0.05, 6000
+    dec = Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, flip_sets=hx, logicals=lz)
+    dev = torch.device("cuda", 0)
+    syn = torch.empty((B, hz.shape[0]), dtype=torch.uint8, device=dev)
+    rd = torch.empty((B, hz.shape[1]), dtype=torch.uint8, device=dev)
+    dec.sample_storage_device(0, p, p, 7, 0, 0, B, syn, rd)
+    rs, rr = syn.cpu().numpy(), rd.cpu().numpy()
+    ref = oracle_lib.decode(hz, 2 * p / 3, rs, method="ms", precision=precision, max_iter=50, ssf=True, gens=hx,
+                            lz=lz, readout=rr, want_llr=False, ssf_impl="fast")
+    for w in (4, 12, 0):
+        dec.set_wave_occupancy(w)
+        out = {k: torch.empty(B, dtype=dt, device=dev) for k, dt in
+               (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
+        dec.decode_device(B, syn=syn, readout=rd, **out)
+        torch.cuda.synchronize()
+        for k in out:
+            assert np.array_equal(out[k].cpu().numpy(), ref[k]), (w, k)
+    with pytest.raises(QdecError):
+        dec.set_wave_occupancy(-1)
