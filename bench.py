@@ -585,8 +585,12 @@ def main():
                 roof["on_chip_bound"] = {
                     "unit": "lds" if lf >= vf else "valu", "lds_busy": lf, "valu_issue": vf,
                     "lds_bank_conflict_ratio": dv.get("lds_bank_conflict_ratio"),
-                    "note": "per-wave LDS traffic per BP iteration (f64): 8 row reads, 2 state writes, "
-                            "14 state gathers, 14 v2c scatters (DESIGN.md §4); HBM frac above is compulsory I/O"}
+                    "note": "per-wave LDS work per BP iteration (f64): 6 ds_read_b128 + 2 ds_read_b64 row reads, "
+                            "2 ds_write_b128 state writes, 14 ds_read_b128 state gathers, 14 ds_write_b64 v2c "
+                            "scatters = 211 LDS-array cycles with bank conflicts by the layout model "
+                            "(tools/dev/ms_conflicts.py; PMC of the previous layout: 225, model 231); valu_issue "
+                            "prices every wave64 VALU op at 2 cycles, the loop's f64 ops take ~4.9, so the f64 pipe "
+                            "is ~0.65 busy at p = 0.1 (DESIGN.md §4); HBM frac above is compulsory I/O"}
         calib = os.path.join(REPO, "profiles", "r03_hbm_calibration")
         if os.path.isdir(calib):
             roof["traffic_calibration"] = {
