@@ -344,7 +344,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
     uint32_t* qt = lct + NLW * GP;                      // [kGenW/2][GP]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint64_t* lzs_lds = reinterpret_cast<uint64_t*>(smem + SsfLds<RG>::table_bytes());
-    const uint64_t* lzs = lz_in_lds(g) ? lzs_lds : g.lz;
+    const uint64_t* lzs = lzs_lds;  // LDS copy when lz_in_lds (lz_word / lz_row_parity)
     uint16_t* invt = reinterpret_cast<uint16_t*>(smem + SsfLds<RG>::table_bytes() + SsfLds<RG>::lz_bytes(g));
     const bool inc = g.g_inv != nullptr;  // incremental local syndromes
     unsigned char* wbase = smem + SsfLds<RG>::shared_bytes(g) + (size_t)wave * SsfLds<RG>::wave_bytes(g);
@@ -588,19 +588,15 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
                 uint64_t Rd[XW];
 #pragma unroll
                 for (int w = 0; w < XW; ++w) Rd[w] = __ballot(xh[w * 64 + lane] & 1) ^ D[w];
+                QDEC_STAMP(8);
                 int f = 0;
 #pragma unroll
                 for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
                     const int r = rr * 64 + lane;
-                    if (r < g.k) {
-                        int par = 0;
-#pragma unroll
-                        for (int w = 0; w < XW; ++w)
-                            if (w < g.lz_words) par += __popcll(lzs[(size_t)r * g.lz_words + w] & Rd[w]);
-                        f |= par & 1;
-                    }
+                    if (r < g.k) f |= lz_row_parity<XW>(g, lzs, r, Rd);
                 }
                 any_fail = __ballot(f) != 0ull;
+                QDEC_STAMP(9);
             }
             if (lane == 0) {
                 if (a.status) a.status[shot] = (uint8_t)(sw == 0 ? 2 : 0);
@@ -631,6 +627,11 @@ static size_t wave_lds_bytes(const DevGraph& g) {
 template <int RG, int XW, int RW>
 static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     const size_t lds = SsfLds<RG>::shared_bytes(g) + kSsfWaves * SsfLds<RG>::wave_bytes(g);
+    if (lds > 64 * 1024) {
+        const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ssf_wave_kernel<RG, XW, RW>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return (int)ea;
+    }
     int per_cu = 0;
     hipError_t e =
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ssf_wave_kernel<RG, XW, RW>, 64 * kSsfWaves, lds);
@@ -647,6 +648,11 @@ static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, 
 template <typename K>
 static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
                              const DecodeArgs& a, int block = 64, int max_per_cu = 0) {
+    if (lds > 64 * 1024) {  // e.g. a large LDS copy of the logicals (lz_in_lds)
+        const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return (int)ea;
+    }
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds);
     if (e != hipSuccess) return (int)e;
@@ -672,6 +678,9 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
 template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
 static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if constexpr (METHOD == 1) {
+        // the fused failure check reads the dense logical table's LDS copy
+        // (lz_in_lds); wave-kernel graphs always have one (n <= 576)
+        if (a.fail && g.k > 0 && !g.lz) return (int)hipErrorInvalidValue;
         const size_t lds = MsLds<T>::template bytes<RC, RV>(g);
         if (a.wave_ctr) {  // ShotSeq's chunk counter
             const hipError_t e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);

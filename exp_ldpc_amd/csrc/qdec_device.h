@@ -366,10 +366,31 @@ __device__ inline void finalize_shot(const DevGraph& g, const DecodeArgs& a, int
 // the next shot's.  The final 1-3 bytes of a buffer whose length is not a
 // multiple of 4 are not covered by a whole dword; the shot that needs them
 // patches them in with byte loads (patch_tail).
-constexpr int kLzLdsBytes = 2048;
+// The wave kernels (one shot per wave: bp_ms_wave_kernel, ssf_wave_kernel)
+// keep the dense logical table in LDS: for their graphs (n <= 576, so at most
+// 9 words per logical) it is at most 41.5 KB, and C2's is 288 B.  Every word
+// is read through an LDS-typed pointer: a generic (flat) load would wait for
+// every vector-memory operation of the wave, i.e. for the next shot's LDS-DMA
+// stage, serialising the stage with the shot (SSF launch at p = 0.032: 8.1 k of
+// 18.7 k ticks per shot), and a global fallback path costs the f64 BP kernel 12
+// VGPRs, past the 168 that fit three waves per SIMD.
+__host__ __device__ inline bool lz_in_lds(const DevGraph& g) { return g.k > 0 && g.lz != nullptr; }
 
-__host__ __device__ inline bool lz_in_lds(const DevGraph& g) {
-    return g.k > 0 && (size_t)g.k * g.lz_words * 8 <= (size_t)kLzLdsBytes;
+using lds_u64 = __attribute__((address_space(3))) const uint64_t;
+__device__ __forceinline__ uint64_t lz_word(const uint64_t* lz_lds, size_t idx) {
+    // volatile: keeps the loop-invariant rows from being hoisted into
+    // registers across the shot loop
+    return ((const volatile lds_u64*)lz_lds)[idx];
+}
+// Parity of popc(Lz[r] & R) for logical row r < g.k.
+template <int NW>
+__device__ __forceinline__ int lz_row_parity(const DevGraph& g, const uint64_t* lz_lds, int r, const uint64_t (&R)[NW]) {
+    const size_t base = (size_t)r * g.lz_words;
+    int par = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i)
+        if (i < g.lz_words) par += __popcll(lz_word(lz_lds, base + i) & R[i]);
+    return par & 1;
 }
 
 template <int RC, int NW>
@@ -384,15 +405,14 @@ struct ShotIo {
     }
     uint8_t* syn;        // [NS*256]     staged syndrome row of the next shot
     uint8_t* rd;         // [2][NR*256]  staged readout rows, by loop parity
-    const uint64_t* lz;  // LDS copy or the global table
+    const uint64_t* lz;  // the LDS copy of the logicals (read with lz_word / lz_row_parity)
     int syn_shift;       // byte offset of the staged syndrome row
     int rd_shift0, rd_shift1;  // ... of the staged readout rows (no dynamic register indexing)
 
     __device__ ShotIo(const DevGraph& g, unsigned char* base) {
         syn = base;
         rd = base + 256 * NS;
-        uint64_t* l = reinterpret_cast<uint64_t*>(base + 256 * (NS + 2 * NR));
-        lz = lz_in_lds(g) ? l : g.lz;
+        lz = reinterpret_cast<const uint64_t*>(base + 256 * (NS + 2 * NR));
         syn_shift = 0;
         rd_shift0 = rd_shift1 = 0;
     }
@@ -494,7 +514,7 @@ __device__ inline void finalize_shot_io(const DevGraph& g, const DecodeArgs& a, 
 #pragma unroll
                 for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
                     const int r = rr * 64 + lane;
-                    if (r < g.k) lpar[rr] ^= __popcll(lzs[(size_t)r * g.lz_words + w0] & word) & 1;
+                    if (r < g.k) lpar[rr] ^= __popcll(lz_word(lzs, (size_t)r * g.lz_words + w0) & word) & 1;
                 }
             }
         }
@@ -539,11 +559,7 @@ __device__ inline int fail_from_words(const DevGraph& g, const DecodeArgs& a, in
     for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
         const int r = rr * 64 + lane;
         if (r < g.k) {
-            int p = 0;
-#pragma unroll
-            for (int w = 0; w < NW; ++w)
-                if (w < g.lz_words) p += __popcll(lzs[(size_t)r * g.lz_words + w] & R[w]);
-            f |= p & 1;
+            f |= lz_row_parity<NW>(g, lzs, r, R);
         }
     }
     return __ballot(f) != 0ull;

@@ -57,4 +57,5 @@ for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
     if shots:
         print(f"SSF p={p} shots={shots} steps/shot={steps/shots:.2f} listed/step={b[5]/max(1,steps):.1f} per-step ticks: "
               f"gather+compact={b[0]/steps:.0f} score={b[1]/steps:.0f} select={b[2]/steps:.0f} apply={b[3]/steps:.0f} | "
-              f"per-shot: load={b[12]/shots:.0f} tail={b[13]/shots:.0f} finalize={b[14]/shots:.0f}", flush=True)
+              f"per-shot: load={b[12]/shots:.0f} tail={b[13]/shots:.0f} fin_words={b[8]/shots:.0f} "
+              f"fin_logicals={b[9]/shots:.0f} fin_stores={b[14]/shots:.0f}", flush=True)
