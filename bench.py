@@ -338,8 +338,9 @@ class Run:
         ev.record(streams[0])
         for st in streams[1:]:
             st.wait_event(ev)
-        for pi in range(len(self.ps)):
-            st = streams[pi % len(streams)]
+        order = range(len(self.ps)) if self.args.point_order == "asc" else range(len(self.ps) - 1, -1, -1)
+        for j, pi in enumerate(order):
+            st = streams[j % len(streams)]
             decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                    status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi],
                                    stream=st.cuda_stream)
@@ -409,6 +410,8 @@ def main():
     ap.add_argument("--wave-occupancy", type=int, default=-1,
                     help="waves per CU of the wave BP kernels in the overlapped phases (qd_graph_set_wave_occupancy); "
                          "-1 = 12 for f64 when the points share the chip over several streams, else the default")
+    ap.add_argument("--point-order", default="asc", choices=["asc", "desc"],
+                    help="launch order of the sweep points in the overlapped phases (desc: highest p first)")
     ap.add_argument("--iso-steps", type=int, default=2, help="isolated (one-stream) steps timing each kernel")
     ap.add_argument("--no-sample-phase", action="store_true", help="skip the sampling+decode phase")
     ap.add_argument("--no-large-code", action="store_true",

@@ -695,6 +695,11 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
             if (g.ms_d3r >= 2) {
+                if constexpr (sizeof(T) == 8) {
+                    if (lean && cap > 8)  // 3 waves per SIMD: the 168-VGPR build
+                        return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 2, 3>, lds, a.B,
+                                                 num_cus, stream, g, a, 64, cap);
+                }
                 if (lean)
                     return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 2>, lds, a.B, num_cus,
                                              stream, g, a, 64, cap);

@@ -73,6 +73,53 @@ __device__ __forceinline__ double max_abs2_f64(double a, double b) {
     return r;
 }
 
+// Sign-bit tests for f64 messages (QDEC_MS_SIGNBIT, default on; LEAN launches
+// only).  ldpc's sign test `v <= 0` equals v's sign bit for every v but +0.
+// The check pass takes its row parity as the XOR of the high dwords (no f64
+// compares) and the variable pass flips a message's sign by the sign bit of the
+// v2c message it sent.  Both differ from the compares only through zero
+// entries, and a zero entry makes the row's m1 zero, so a row with m1 == 0
+// (rare; a divergent branch) takes the parity from the compares and gives m2
+// (the magnitude its zero entries select) the sign that makes the variable
+// side's sign bit test exact: the parity, flipped when the zeros are +0.  A
+// row holding both +0 and -0 has m2 = 0, where only the sign of a zero message
+// is left open, which changes no `<= 0` test, no magnitude and no hard
+// decision (only the sign of an exactly-zero posterior, which LEAN launches do
+// not output).
+#ifndef QDEC_MS_SIGNBIT
+#define QDEC_MS_SIGNBIT 1
+#endif
+__device__ __forceinline__ uint32_t f64_hi(double x) { return (uint32_t)((unsigned long long)__double_as_longlong(x) >> 32); }
+// x with its sign bit XORed with bit 31 of m: one v_bitop3_b32 on the high
+// dword (table 0x6c = (src0 & src2) ^ src1)
+__device__ __forceinline__ double f64_xor_sign(double x, uint32_t m) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32(m, (uint32_t)(b >> 32), 0x80000000u, 0x6c);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | (uint32_t)b));
+}
+
+// The zero-row fix-up of the sign-bit check pass (a call: its registers stay
+// out of the BP loop's allocation).  `row`: the check's v2c row, `par`: its
+// syndrome bit, `sp`: its (m1, m2) state slot, written with the sign-bit parity.
+// m1's sign becomes the parity by ldpc's compares; m2 (the magnitude the row's
+// zero entries select) gets the parity flipped when those zeros are +0, so that
+// the variable side's sign-bit test gives parity ^ (v <= 0) for them too.
+using lds_f64 = __attribute__((address_space(3))) double;
+template <int DRC>
+__device__ __noinline__ void ms_zero_row_fix(lds_f64* row, bool par, lds_f64* sp) {
+    bool pz = false;
+#pragma unroll 1
+    for (int j = 0; j < DRC; ++j) {
+        const double w = row[j];
+        par ^= w <= 0.0;
+        pz |= __double_as_longlong(w) == 0ll;  // +0
+    }
+    const uint32_t hx = par ? 0x80000000u : 0u;
+    const uint32_t h2 = pz ? hx ^ 0x80000000u : hx;
+    sp[0] = f64_xor_sign(fabs(sp[0]), hx);
+    sp[1] = f64_xor_sign(fabs(sp[1]), h2);
+}
+
 // (smallest, second smallest) of |v[B]| .. |v[E-1]|, counted with multiplicity
 // (ldpc's leave-one-out minima need exactly these two).  Leaves are pairs
 // (min, max) or a single value (hi = none); merge(A, B) = (min(A.lo, B.lo),
@@ -201,8 +248,12 @@ struct ShotSeq {
 // D3R: leading variable rounds whose slots all have degree <= 3.
 // f64: launched at 2 waves per SIMD (launch_bp_wave caps the grid; measured
 // faster than 3), so the register budget is 256; f32: 4 waves (<= 128 VGPRs).
-template <typename T, int RC, int RV, int DRC, bool DEFER, bool LEAN, int D3R>
-__global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(DevGraph g, DecodeArgs a) {
+// OCC: waves per SIMD the registers are budgeted for (0 = the default above).
+// The f64 LEAN kernel also comes as OCC = 3 (<= 168 VGPRs, a few dwords of the
+// per-shot epilogue spilled), launched when a handle asks for more than 8 f64
+// waves per CU (qd_graph_set_wave_occupancy: the bench's concurrent points).
+template <typename T, int RC, int RV, int DRC, bool DEFER, bool LEAN, int D3R, int OCC = 0>
+__global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void bp_ms_wave_kernel(DevGraph g, DecodeArgs a) {
     static_assert(DRC <= kDR, "compute width exceeds the LDS row");
     static_assert(D3R <= RV, "degree rounds");
     using V2 = __attribute__((ext_vector_type(2))) T;
@@ -360,6 +411,7 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
         for (; !kSkipBp && !skip && it <= a.max_iter; ++it) {
             const T alpha = alpha_bits<T>(it, a.ms_scaling);
             // ---- check pass: state (m1, m2) with the parity in both signs ----
+            uint32_t zrows = 0;  // rows holding a zero entry (sign-bit parity inexact)
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) {
                 const int i = min(rc * 64 + lane, m);  // pad check lanes share the Big row m
@@ -384,14 +436,45 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
                     m1 = t.lo;
                     m2 = t.hi;
                 }
-#pragma unroll
-                for (int k = 0; k < DRC; ++k)
-                    par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign (s_xor of compare masks)
-                // both minima carry the parity in their sign bit (they are >= +0)
                 V2 s2;
-                s2.x = par ? -m1 : m1;
-                s2.y = par ? -m2 : m2;
+                constexpr bool SB = sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT;
+                if constexpr (SB) {
+                    // sign-canonical row: the parity is the XOR of the sign bits
+                    uint32_t hx = par ? 0x80000000u : 0u;
+                    int k = 0;
+#pragma unroll
+                    for (; k + 1 < DRC; k += 2) hx = __builtin_amdgcn_bitop3_b32(hx, f64_hi(v[k]), f64_hi(v[k + 1]), 0x96);
+                    if (k < DRC) hx ^= f64_hi(v[k]);
+                    // m1, m2 >= +0: the XOR of the parity bit sets their sign bit
+                    s2.x = f64_xor_sign(m1, hx);
+                    s2.y = f64_xor_sign(m2, hx);
+                    if (m1 == (T)0) zrows |= 1u << rc;  // a zero entry: fixed below
+                } else {
+#pragma unroll
+                    for (int k = 0; k < DRC; ++k)
+                        par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign (s_xor of compare masks)
+                    // both minima carry the parity in their sign bit (they are >= +0)
+                    s2.x = par ? -m1 : m1;
+                    s2.y = par ? -m2 : m2;
+                }
                 *reinterpret_cast<V2*>(st + 2 * sslot[rc]) = s2;
+            }
+            if constexpr (sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT) {
+#ifdef QDEC_STAMPS
+                {  // dev counters: wave-iterations with a zero row, zero-row lanes
+                    const unsigned long long zb = __ballot(zrows != 0u);
+                    QDEC_COUNT(13, zb != 0ull);
+                    QDEC_COUNT(14, __popcll(zb));
+                }
+#endif
+                if (__ballot(zrows != 0u)) {  // rare (wave-uniform): rows with a zero entry, parity by the compares
+                    asm volatile("" ::: "memory");  // re-read the row and the state just written
+#pragma unroll
+                    for (int rc = 0; rc < RC; ++rc)
+                        if ((zrows >> rc) & 1u)
+                            ms_zero_row_fix<DRC>((lds_f64*)(v2c + min(rc * 64 + lane, m) * DRS), sbit[rc],
+                                                 (lds_f64*)(st + 2 * sslot[rc]));
+                }
             }
             wave_lds_sync();
 
@@ -429,8 +512,13 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 4 : 2) void bp_ms_wave_kernel(
                 for (int k = 0; k < kDC; ++k) {
                     if (k < KD) {
                         const V2 yk = y[k] * alpha;
-                        c[k].x = (vp[p][k].x <= (T)0) ? -yk.x : yk.x;
-                        c[k].y = (vp[p][k].y <= (T)0) ? -yk.y : yk.y;
+                        if constexpr (sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT) {
+                            c[k].x = f64_xor_sign(yk.x, f64_hi(vp[p][k].x));
+                            c[k].y = f64_xor_sign(yk.y, f64_hi(vp[p][k].y));
+                        } else {
+                            c[k].x = (vp[p][k].x <= (T)0) ? -yk.x : yk.x;
+                            c[k].y = (vp[p][k].y <= (T)0) ? -yk.y : yk.y;
+                        }
                     }
                 }
                 V2 pre[kDC];

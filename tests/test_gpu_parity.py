@@ -422,14 +422,15 @@ def test_lds_kernel_ssf_fold(gpu_available, oracle_lib, code225, monkeypatch):
         assert np.array_equal(got[key], ref[key]), key
 
 
-@pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision):
+@pytest.mark.parametrize("precision,occupancy", [("f64", 0), ("f64", 12), ("f32", 0)])
+def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occupancy):
     """The benchmarked instantiation (bp_ms_wave_kernel<.., LEAN=true, ..>, chosen
     when x / corr / llr are all null) pinned bit-exactly: exactly bench.py's
     decode_device call (syn + readout in; iters, status, ssf_steps, fail out) at
     all 9 sweep points, 4096 device-sampled shots each (bench.py's sampler
     streams, shot offset of its step 3), f64 headline and f32 variant, every
-    output compared with the oracle on the same shots."""
+    output compared with the oracle on the same shots.  f64 also at 12 waves per
+    CU (bench.py's overlapped phases: the 3-waves-per-SIMD build)."""
     import torch
     from exp_ldpc_amd.decoder import Decoder
     code = load_code("hgp_12_3_4_s1234")
@@ -439,6 +440,8 @@ def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision):
     for pi, p in enumerate(np.geomspace(1e-3, 1e-1, 9)):
         dec = Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0,
                       flip_sets=hx, logicals=lz)
+        if occupancy:
+            dec.set_wave_occupancy(occupancy)
         syn = torch.empty((B, hz.shape[0]), dtype=torch.uint8, device=dev)
         rd = torch.empty((B, hz.shape[1]), dtype=torch.uint8, device=dev)
         dec.sample_storage_device(0, p, p, seed, pi, shot0, B, syn, rd)
@@ -514,3 +517,37 @@ def test_wave_occupancy_does_not_change_results(gpu_available, oracle_lib, preci
             assert np.array_equal(out[k].cpu().numpy(), ref[k]), (w, k)
     with pytest.raises(QdecError):
         dec.set_wave_occupancy(-1)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_lean_zero_messages(gpu_available, oracle_lib, precision):
+    """Exact zero messages on the LEAN kernel.  The f64 LEAN kernel reads ldpc's
+    sign test `v <= 0` from sign bits (QDEC_MS_SIGNBIT) and takes a rare path for
+    check rows holding a zero entry (+0 or -0).  Priors of exactly 0 (p = 0.5:
+    log(1) = +0) put +0 messages into the rows from iteration 1; a mix of p = 0.5
+    and p = 0.5 +- tiny steps gives +0, -0-producing sums and sign changes, and all
+    columns at 0.5 makes every row all-zero.  Iterations, status, SSF steps and
+    failure flags equal the oracle's (compare-based) in every case."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    code = load_code("hgp_12_3_4_s1234")
+    hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
+    rng = np.random.default_rng(5)
+    B, n = 3000, hz.shape[1]
+    e = (rng.random((B, n)) < 0.03).astype(np.uint8)
+    syn = np.ascontiguousarray(((hz @ e.T).T % 2).astype(np.uint8))
+    rd = (e ^ (rng.random((B, n)) < 0.01)).astype(np.uint8)
+    dev = torch.device("cuda", 0)
+    cases = (np.where(np.arange(n) % 5 == 0, 0.5, 0.02),
+             np.where(np.arange(n) % 3 == 0, 0.5, np.where(np.arange(n) % 3 == 1, 0.3, 0.7)),
+             np.full(n, 0.5))
+    for ci, probs in enumerate(cases):
+        dec = Decoder(hz, probs, method="ms", precision=precision, max_iter=25, flip_sets=hx, logicals=lz)
+        out = {k: torch.empty(B, dtype=dt, device=dev) for k, dt in
+               (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
+        dec.decode_device(B, syn=torch.from_numpy(syn).to(dev), readout=torch.from_numpy(rd).to(dev), **out)
+        torch.cuda.synchronize()
+        ref = oracle_lib.decode(hz, probs, syn, method="ms", precision=precision, max_iter=25, ssf=True, gens=hx,
+                                lz=lz, readout=rd, want_llr=False, ssf_impl="fast")
+        for k in out:
+            assert np.array_equal(out[k].cpu().numpy(), ref[k]), (ci, k)

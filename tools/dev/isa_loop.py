@@ -20,7 +20,7 @@ for i, l in enumerate(body):
     if m and m.group(2) in labels and labels[m.group(2)] < i:
         a = labels[m.group(2)]
         seg = body[a:i + 1]
-        if any("v_med3" in s for s in seg) and (best is None or i - a < best[1] - best[0]):
+        if any(("v_med3" in s or "v_min_f64" in s) for s in seg) and (best is None or i - a < best[1] - best[0]):
             best = (a, i)
 a, b = best
 ins = [l.strip() for l in body[a:b + 1] if l.startswith("\t") and not l.strip().startswith((";", "."))]
