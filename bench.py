@@ -559,7 +559,8 @@ def main():
         kname = "qdec::bp_ms_wave_kernel<" + ("double" if args.precision == "f64" else "float")
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": kname + ", 2, 4, 7, true, true, 2> (BP min-sum, lean outputs, queues BP failures)",
+                "kernel": kname + ", 2, 4, 7, true, true, 2, 0> (BP min-sum, lean outputs, queues BP failures; the "
+                          "overlapped phases run its 3-waves-per-SIMD build <..., 2, 3>)",
                 "avg_launch_ms": float(bp_ms.mean()), "launches": int(bp_ms.size),
                 "timing": "HIP events recorded by the library on the launch stream around each kernel, "
                           "isolated phase (one stream)",
@@ -592,8 +593,9 @@ def main():
                             "2 ds_write_b128 state writes, 14 ds_read_b128 state gathers, 14 ds_write_b64 v2c "
                             "scatters = 211 LDS-array cycles with bank conflicts by the layout model "
                             "(tools/dev/ms_conflicts.py; PMC of the previous layout: 225, model 231); valu_issue "
-                            "prices every wave64 VALU op at 2 cycles, the loop's f64 ops take ~4.9, so the f64 pipe "
-                            "is ~0.65 busy at p = 0.1 (DESIGN.md §4); HBM frac above is compulsory I/O"}
+                            "prices every wave64 VALU op at 2 cycles, the loop's f64 ops take ~4.9 (98 of them per "
+                            "iteration since the sign-bit check pass, 124 before; DESIGN.md §3.1, §4); HBM frac "
+                            "above is compulsory I/O"}
         calib = os.path.join(REPO, "profiles", "r03_hbm_calibration")
         if os.path.isdir(calib):
             roof["traffic_calibration"] = {

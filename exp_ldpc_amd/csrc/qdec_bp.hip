@@ -305,10 +305,20 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 //   4. the flip updates the residual (u32 per check in LDS) and hard decision.
 // Key (int32): score << 15 | (127 - g) << 8; |score| <= 32*840 < 2^15, g < 128.
 constexpr int kSsfWaves = 4;
+#ifndef QDEC_SSF_INV_INIT
+#define QDEC_SSF_INV_INIT 0  // 1: first-step local syndromes from the inverse table (measured no faster)
+#endif
 #ifndef QDEC_SSF_OCC
 #define QDEC_SSF_OCC 4  // minimum waves per SIMD the SSF kernel is compiled for
 #endif
 
+// residual bit per check: u32 (default) or u8 (QDEC_SSF_RES8: 3/4 less LDS
+// per wave, so five 4-wave workgroups fit a CU; measured with QDEC_SSF_OCC=5)
+#ifdef QDEC_SSF_RES8
+using SsfRes = uint8_t;
+#else
+using SsfRes = uint32_t;
+#endif
 template <int RG>
 struct SsfLds {
     static constexpr int GP = 64 * RG;
@@ -323,8 +333,11 @@ struct SsfLds {
     __host__ __device__ static size_t shared_bytes(const DevGraph& g) { return table_bytes() + lz_bytes(g) + inv_bytes(g); }
     // residual, cached keys, listed local syndromes, current local syndromes,
     // flipped-check list, listed generators, hard decision, staged queue entries
+    __host__ __device__ static size_t res_bytes(const DevGraph& g) {
+        return (((size_t)g.m_pad + 64) * sizeof(SsfRes) + 15) / 16 * 16;
+    }
     __host__ __device__ static size_t wave_bytes(const DevGraph& g) {
-        return (((size_t)g.m_pad + 64) * 4 + (size_t)GP * 4 * 3 + kGenLC * 4 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16 +
+        return res_bytes(g) + ((size_t)GP * 4 * 3 + kGenLC * 4 + GP + (size_t)g.n_pad + 64 + 15) / 16 * 16 +
                256 * kStage;
     }
 };
@@ -348,8 +361,8 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
     uint16_t* invt = reinterpret_cast<uint16_t*>(smem + SsfLds<RG>::table_bytes() + SsfLds<RG>::lz_bytes(g));
     const bool inc = g.g_inv != nullptr;  // incremental local syndromes
     unsigned char* wbase = smem + SsfLds<RG>::shared_bytes(g) + (size_t)wave * SsfLds<RG>::wave_bytes(g);
-    uint32_t* sres = reinterpret_cast<uint32_t*>(wbase);      // [m_pad + 64] residual (pads stay 0)
-    int* key = reinterpret_cast<int*>(sres + g.m_pad + 64);   // [GP] cached best keys
+    SsfRes* sres = reinterpret_cast<SsfRes*>(wbase);          // [m_pad + 64] residual (pads stay 0)
+    int* key = reinterpret_cast<int*>(wbase + SsfLds<RG>::res_bytes(g));  // [GP] cached best keys
     uint32_t* slt = reinterpret_cast<uint32_t*>(key + GP);    // [GP] local syndromes of listed gens
     uint32_t* slc = slt + GP;                                 // [GP] current local syndromes (inc)
     uint32_t* clist = slc + GP;                               // [kGenLC] checks flipped by a step (inc)
@@ -412,12 +425,9 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
         wait_vmem<1>();
         const uint64_t* ew = reinterpret_cast<const uint64_t*>(ent + 256 * sb);
         const int64_t shot = (int64_t)ew[0];
-        uint64_t X[XW], R[RW], D[XW];
+        uint64_t X[XW], R[RW];
 #pragma unroll
-        for (int w = 0; w < XW; ++w) {
-            X[w] = ew[1 + w];
-            D[w] = ew[1 + XW + RW + w];
-        }
+        for (int w = 0; w < XW; ++w) X[w] = ew[1 + w];
 #pragma unroll
         for (int w = 0; w < RW; ++w) R[w] = ew[1 + XW + w];
         wait_lds();
@@ -432,8 +442,36 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
 #pragma unroll
         for (int w = 0; w < RW; ++w) {
             const int i = w * 64 + lane;
-            sres[i] = i < m ? (uint32_t)((R[w] >> lane) & 1) : 0u;
+            sres[i] = i < m ? (SsfRes)((R[w] >> lane) & 1) : (SsfRes)0;
             sw += __popcll(R[w]);
+        }
+        // QDEC_SSF_INV_INIT (incremental mode): the first step's local syndromes
+        // from the inverse table too, fanned out from the violated checks (listed
+        // into slt, which step 1 overwrites) instead of gathered bit by bit (up
+        // to kGenLC LDS reads per generator).  Bit-exact, measured no faster
+        // (isolated SSF sum 6.79-6.83 vs 6.74-6.76 ms), so off.
+        constexpr bool kInvInit = QDEC_SSF_INV_INIT && RW <= RG;  // slt holds GP >= 64 * RW check ids
+        const bool inv_init = inc && kInvInit;
+        if (inv_init) {
+            int nv = 0;
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg) slc[rg * 64 + lane] = 0u;
+#pragma unroll
+            for (int w = 0; w < RW; ++w) {
+                const int i = w * 64 + lane;
+                const bool v = i < m && ((R[w] >> lane) & 1);
+                const unsigned long long bal = __ballot(v);
+                if (v)
+                    slt[nv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = (uint32_t)i;
+                nv += __popcll(bal);
+            }
+            wave_lds_sync();
+            const int npair = nv << g.g_invl;
+            for (int pr = lane; pr < npair; pr += 64) {
+                const uint32_t e = invt[(slt[pr >> g.g_invl] << g.g_invl) + (pr & (g.g_invd - 1))];
+                if (e != 0xffffu) atomicXor(&slc[e & 0xff], 1u << (e >> 8));
+            }
         }
         wave_lds_sync();
         uint32_t slo[RG];
@@ -448,13 +486,13 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             for (int rg = 0; rg < RG; ++rg) {
                 const int gi = rg * 64 + lane;
                 uint32_t sl = 0;
-                if (first || !inc) {
+                if (!inc || (first && !inv_init)) {
 #pragma unroll
                     for (int wq = 0; wq < NLW; ++wq) {
                         if (wq < nlcw) {
                             const uint32_t pk = lct[wq * GP + gi];
 #pragma unroll
-                            for (int bb = 0; bb < 4; ++bb) sl |= sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
+                            for (int bb = 0; bb < 4; ++bb) sl |= (uint32_t)sres[(pk >> (8 * bb)) & 0xff] << (wq * 4 + bb);
                         }
                     }
                     if (inc) slc[gi] = sl;
@@ -558,7 +596,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             if (lane < kGenLC && ((fm >> lane) & 1)) {
                 const uint32_t wv = lct[(lane >> 2) * GP + gsel];
                 const uint32_t c = (wv >> (8 * (lane & 3))) & 0xff;
-                sres[c] ^= 1u;
+                sres[c] ^= (SsfRes)1;
                 clist[__builtin_popcount(fm & ((1u << lane) - 1u))] = c;
             }
             if (inc) {
@@ -585,9 +623,11 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
         if (lean_fin) {
             int any_fail = 0;
             if (want_fail) {  // readout words came with the queue entry
+                // the readout words are re-read from this slot's staging buffer
+                // (restaged only by the next slot), not held across the steps
                 uint64_t Rd[XW];
 #pragma unroll
-                for (int w = 0; w < XW; ++w) Rd[w] = __ballot(xh[w * 64 + lane] & 1) ^ D[w];
+                for (int w = 0; w < XW; ++w) Rd[w] = __ballot(xh[w * 64 + lane] & 1) ^ ew[1 + XW + RW + w];
                 QDEC_STAMP(8);
                 int f = 0;
 #pragma unroll

@@ -310,25 +310,32 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     io.init(g, lane);
     ShotSeq seq(a, lane);
     int64_t shot = seq.next(lane);
-    io.stage(g, a, shot, 0, lane);
+    typename Io::Shift sh = io.stage(g, a, shot, 0, 0, lane);  // row offsets of `shot`'s stage
     int64_t nxt = seq.next(lane);
+    int64_t nxt2 = 0;  // the shot after nxt (stage depth 2)
+    typename Io::Shift sh1;  // ... of nxt's (stage depth 2)
+    if constexpr (Io::kDepth == 2) {
+        sh1 = io.stage(g, a, nxt, 1, 1, lane);
+        nxt2 = seq.next(lane);
+    }
     wave_lds_sync();
 
-    int buf = 0;
+    int sb = 0, buf = 0;  // syndrome / readout staging buffers of `shot`
     QDEC_STAMP_DECL
 #ifdef QDEC_STAMPS
     const unsigned long long qdec_t0 = __builtin_amdgcn_s_memtime(), qdec_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (; shot < a.B; buf ^= 1) {
-        // ---- syndrome (staged one shot ahead: at least the NR readout loads of
-        // the same stage are younger); then stage the next shot ----
+    for (; shot < a.B;) {
+        // ---- syndrome (staged kDepth shots ahead: at least the NR readout loads
+        // of the same stage and the later stages are younger); then stage the
+        // shot kDepth ahead ----
         QDEC_STAMP(5);
-        wait_vmem<Io::NR>();
-        Io::patch_tail(a.syn, a.B, m, shot, io.syn, io.syn_shift, lane);
+        wait_vmem<Io::kWaitSyn>();
+        Io::patch_tail(a.syn, a.B, m, shot, io.syn_area(sb), sh.s, lane);
         wave_lds_sync();
         QDEC_STAMP(0);
         bool sbit[RC];  // lane masks: parity work stays on the scalar unit
-        const uint8_t* srow = io.syn_row();
+        const uint8_t* srow = io.syn_area(sb) + sh.s;
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) {
             const int i = rc * 64 + lane;
@@ -336,7 +343,8 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         }
         wait_lds();
         const int64_t nn = seq.next(lane);  // any counter request is older than the stage
-        io.stage(g, a, nxt, buf ^ 1, lane);
+        const typename Io::Shift shn = Io::kDepth == 2 ? io.stage(g, a, nxt2, sb, buf == 0 ? 2 : buf - 1, lane)
+                                                       : io.stage(g, a, nxt, 0, buf ^ 1, lane);
         if (!LEAN && a.syn_flags) {
             const bool use_b = (a.syn_flags & 1) && a.base;
             const bool use_r = (a.syn_flags & 2) && a.readout;
@@ -569,12 +577,12 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         QDEC_STAMP(2);
         QDEC_COUNT(8, iters);
         QDEC_COUNT(9, 1);
-        // this shot's readout: wait before any store of this shot, so the kStaged
-        // most recent vector-memory operations are exactly the next shot's stage
+        // this shot's readout: wait before any store of this shot, so the
+        // kWaitRd most recent vector-memory operations are the later shots' stages
         const bool need_rd = a.readout && a.fail && g.k > 0;  // the SSF queue carries it too
         if (need_rd) {
-            wait_vmem<Io::kStaged>();
-            Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd_area(buf), io.rd_shift(buf), lane);
+            wait_vmem<Io::kWaitRd>();
+            Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd_area(buf), sh.r, lane);
         }
         if (lane == 0 && a.iters) a.iters[shot] = iters;
         // hard decision by column (slot order -> xh[column])
@@ -593,7 +601,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         if (DEFER && !conv) {
             if (LEAN || a.q_packed) {  // LEAN launches always use the packed queue
                 uint64_t xw[RV], rw[RC], dw[RV];
-                const uint8_t* rrow = io.rd_row(buf);
+                const uint8_t* rrow = io.rd_area(buf) + sh.r;
 #pragma unroll
                 for (int w = 0; w < RV; ++w) {
                     const int q = w * 64 + lane;
@@ -623,7 +631,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
                 uint64_t Xc[RV];  // hard decision by column
 #pragma unroll
                 for (int w = 0; w < RV; ++w) Xc[w] = __ballot(xh[w * 64 + lane] & 1);
-                any_fail = fail_from_words<RV, !LEAN>(g, a, shot, lane, Xc, io.rd_row(buf), io.lz);
+                any_fail = fail_from_words<RV, !LEAN>(g, a, shot, lane, Xc, io.rd_area(buf) + sh.r, io.lz);
             }
             if (lane == 0) {
                 if (a.status) a.status[shot] = (uint8_t)(conv ? 3 : 0);
@@ -631,12 +639,23 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
                 if (a.fail) a.fail[shot] = (uint8_t)any_fail;
             }
         } else {
-            finalize_shot_io(g, a, shot, xh, conv, conv, 0, lane, io.rd_row(buf), io.lz);
+            finalize_shot_io(g, a, shot, xh, conv, conv, 0, lane, io.rd_area(buf) + sh.r, io.lz);
         }
         wave_lds_sync();
         QDEC_STAMP(4);
         shot = nxt;
-        nxt = nn;
+        if constexpr (Io::kDepth == 2) {
+            nxt = nxt2;
+            nxt2 = nn;
+            sh = sh1;
+            sh1 = shn;
+            sb ^= 1;
+            buf = buf == 2 ? 0 : buf + 1;
+        } else {
+            nxt = nn;
+            sh = shn;
+            buf ^= 1;
+        }
     }
 #ifdef QDEC_STAMPS
     QDEC_COUNT(10, __builtin_amdgcn_s_memtime() - qdec_t0);

@@ -393,28 +393,45 @@ __device__ __forceinline__ int lz_row_parity(const DevGraph& g, const uint64_t* 
     return par & 1;
 }
 
+#ifndef QDEC_STAGE_DEPTH
+#define QDEC_STAGE_DEPTH 1
+#endif
 template <int RC, int NW>
 struct ShotIo {
     static constexpr int NS = (64 * RC + 3 + 255) / 256;  // syndrome glds per stage
     static constexpr int NR = (64 * NW + 3 + 255) / 256;  // readout glds per stage
     static constexpr int kStaged = NS + NR;
+    // shots staged ahead (QDEC_STAGE_DEPTH): the syndrome of shot k+D is staged
+    // when shot k starts, so a short shot (a zero syndrome at low p) waits for
+    // HBM once per D shots; D syndrome and D + 1 readout buffers
+    static constexpr int kDepth = QDEC_STAGE_DEPTH;
+    static_assert(kDepth == 1 || kDepth == 2, "stage depth");
+    static constexpr int kSynBufs = kDepth, kRdBufs = kDepth + 1;
+    // vmcnt at the loop top (this shot's syndrome landed: its readout loads and
+    // the D - 1 later stages are younger) and before the readout is read (the D
+    // later stages are younger); stores and counter atomics in between only
+    // make either wait stricter
+    static constexpr int kWaitSyn = NR + (kDepth - 1) * kStaged;
+    static constexpr int kWaitRd = kDepth * kStaged;
     __host__ __device__ static size_t bytes(const DevGraph& g) {
-        size_t b = 256 * (size_t)(NS + 2 * NR);
+        size_t b = 256 * (size_t)(NS * kSynBufs + NR * kRdBufs);
         if (lz_in_lds(g)) b += ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16;
         return b;
     }
-    uint8_t* syn;        // [NS*256]     staged syndrome row of the next shot
-    uint8_t* rd;         // [2][NR*256]  staged readout rows, by loop parity
+    uint8_t* syn;        // [kSynBufs][NS*256]  staged syndrome rows
+    uint8_t* rd;         // [kRdBufs][NR*256]   staged readout rows
     const uint64_t* lz;  // the LDS copy of the logicals (read with lz_word / lz_row_parity)
-    int syn_shift;       // byte offset of the staged syndrome row
-    int rd_shift0, rd_shift1;  // ... of the staged readout rows (no dynamic register indexing)
+    // byte offsets of a staged shot's rows inside their buffers; the kernel
+    // rotates them with the shot indices (a per-buffer array selected by a
+    // loop-carried index would live in scratch)
+    struct Shift {
+        int s = 0, r = 0;
+    };
 
     __device__ ShotIo(const DevGraph& g, unsigned char* base) {
         syn = base;
-        rd = base + 256 * NS;
-        lz = reinterpret_cast<const uint64_t*>(base + 256 * (NS + 2 * NR));
-        syn_shift = 0;
-        rd_shift0 = rd_shift1 = 0;
+        rd = base + 256 * NS * kSynBufs;
+        lz = reinterpret_cast<const uint64_t*>(base + 256 * (NS * kSynBufs + NR * kRdBufs));
     }
     __device__ void init(const DevGraph& g, int lane) {
         if (lz_in_lds(g)) {
@@ -452,14 +469,15 @@ struct ShotIo {
         }
         return (int)(start & 3);
     }
-    // exactly kStaged LDS-DMA loads: syndrome and readout rows of `shot` (shot 0 past B)
-    __device__ void stage(const DevGraph& g, const DecodeArgs& a, int64_t shot, int buf, int lane) {
+    // exactly kStaged LDS-DMA loads: syndrome and readout rows of `shot` (shot 0
+    // past B) into syndrome buffer sb and readout buffer rb
+    __device__ Shift stage(const DevGraph& g, const DecodeArgs& a, int64_t shot, int sb, int rb, int lane) const {
         if (shot >= a.B) shot = 0;
         const uint8_t* dummy = reinterpret_cast<const uint8_t*>(g.col_idx);
-        syn_shift = stage_row<NS>(a.syn, a.B, g.m, shot, syn, lane, dummy);
-        const int sh = stage_row<NR>(a.readout, a.B, g.n_data, shot, rd + 256 * NR * buf, lane, dummy);
-        if (buf) rd_shift1 = sh;
-        else rd_shift0 = sh;
+        Shift sh;
+        sh.s = stage_row<NS>(a.syn, a.B, g.m, shot, syn_area(sb), lane, dummy);
+        sh.r = stage_row<NR>(a.readout, a.B, g.n_data, shot, rd_area(rb), lane, dummy);
+        return sh;
     }
     // bytes [total_dw*4, B*len) of the last row (only when B*len % 4 != 0), after the row's wait
     __device__ static void patch_tail(const uint8_t* buf, int64_t B, int len, int64_t row, uint8_t* dst, int shift,
@@ -470,10 +488,8 @@ struct ShotIo {
         const int64_t q = covered + lane;
         if (q < total && q >= start) dst[shift + (q - start)] = buf[q];
     }
-    __device__ uint8_t* syn_row() const { return syn + syn_shift; }
-    __device__ int rd_shift(int buf) const { return buf ? rd_shift1 : rd_shift0; }
-    __device__ uint8_t* rd_area(int buf) const { return rd + 256 * NR * buf; }
-    __device__ const uint8_t* rd_row(int buf) const { return rd_area(buf) + rd_shift(buf); }
+    __device__ uint8_t* syn_area(int sb) const { return syn + 256 * NS * sb; }
+    __device__ uint8_t* rd_area(int rb) const { return rd + 256 * NR * rb; }
 };
 
 // Waits until at most N of this wave's vector-memory operations (LDS-DMA loads

@@ -186,7 +186,9 @@ int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
  * several decodes running concurrently on different streams: the bench's
  * 9-stream sweep measured 82-83 M shots/s at 12 f64 waves per CU against 80 M
  * at 8, while a lone f64 decode at 12 is slower (p = 0.1: 9.3 vs 7.1 ms per 2^18
- * shots).  Results are identical at every setting.  No reference counterpart. */
+ * shots).  A request above 8 f64 waves per CU launches the kernel's build for
+ * 3 waves per SIMD (the f64 LEAN kernel otherwise needs 172 VGPRs, which fit
+ * only 2).  Results are identical at every setting.  No reference counterpart. */
 int qd_graph_set_wave_occupancy(qd_graph* g, int32_t waves_per_cu);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
 

@@ -9,7 +9,9 @@ of the headline precision in this order: warmup steps + timed steps (phase 1,
 overlapped streams), isolated steps (phase 3, one stream), sampling + decode
 steps (phase 4, one stream); the variant precision's kernels are a different
 template instantiation: warmup + timed (phase 2), isolated (phase 3).  Dispatches
-of one kernel name, sorted by start time, therefore split by count.
+of one kernel name, sorted by start time, therefore split by count.  When the
+overlapped phase runs the 3-waves-per-SIMD build (a distinct instantiation,
+OCC = 3), that name is phase 1 and the default build holds phases 3 and 4.
 """
 from __future__ import annotations
 
@@ -43,7 +45,14 @@ def main():
             # ssf kernels of both precisions share one name: headline phases first
             n1 = (W + K) * P
             phases = {}
-            if headline or ssf:
+            occ3 = headline and name.split(">(")[0].endswith(", 3")
+            if occ3:  # the 3-waves-per-SIMD build runs only in the overlapped phase (12 waves per CU)
+                phases["1_overlapped"] = ms
+            elif headline and any(k != name and ("bp_ms_wave_kernel<" + head) in k and k.split(">(")[0].endswith(", 3")
+                                  for k in by):  # its default build: isolated + sampling phases only
+                phases["3_isolated"] = ms[:iso * P]
+                phases["4_sample_decode"] = ms[iso * P:]
+            elif headline or ssf:
                 phases["1_overlapped"] = ms[:n1]
                 phases["3_isolated"] = ms[n1:n1 + iso * P]
                 rest = ms[n1 + iso * P:]
@@ -64,7 +73,7 @@ def main():
             res["kernels"][name] = {"all": {"dispatches": len(ms), "avg_ms": sum(ms) / len(ms), "sum_ms": sum(ms)}}
     rf = b["roofline"]
     for name, ph in res["kernels"].items():
-        if ("bp_ms_wave_kernel<" + head) in name:
+        if ("bp_ms_wave_kernel<" + head) in name and "3_isolated" in ph:
             r = ph["3_isolated"]["avg_ms"]
             res["compare"] = {"kernel": name, "bench_hip_event_avg_ms": rf["avg_launch_ms"], "rocprof_avg_ms": r,
                               "rel_diff": (r - rf["avg_launch_ms"]) / rf["avg_launch_ms"]}
