@@ -308,12 +308,21 @@ constexpr int kSsfWaves = 4;
 #ifndef QDEC_SSF_INV_INIT
 #define QDEC_SSF_INV_INIT 0  // 1: first-step local syndromes from the inverse table (measured no faster)
 #endif
+// Registers are budgeted for 5 waves per SIMD (<= 96 VGPRs, ~40 dwords of the
+// shot setup / finalisation spilled): with the u8 residual (QDEC_SSF_RES8) five
+// 4-wave workgroups fit a CU's LDS.  Measured against 4 per SIMD with the u32
+// residual, interleaved: isolated SSF sum 6.57-6.59 vs 6.76-6.78 ms, headline
+// 87.7-89.2 vs 85.8-86.5 M shots/s (the smaller LDS footprint also co-resides
+// better with the concurrent BP kernels).
 #ifndef QDEC_SSF_OCC
-#define QDEC_SSF_OCC 4  // minimum waves per SIMD the SSF kernel is compiled for
+#define QDEC_SSF_OCC 5  // minimum waves per SIMD the SSF kernel is compiled for
+#endif
+#ifndef QDEC_SSF_RES32
+#define QDEC_SSF_RES8
 #endif
 
-// residual bit per check: u32 (default) or u8 (QDEC_SSF_RES8: 3/4 less LDS
-// per wave, so five 4-wave workgroups fit a CU; measured with QDEC_SSF_OCC=5)
+// residual bit per check: u8 (QDEC_SSF_RES8, the default: 3/4 less LDS per wave
+// than u32, so five 4-wave workgroups fit a CU) or u32 (QDEC_SSF_RES32)
 #ifdef QDEC_SSF_RES8
 using SsfRes = uint8_t;
 #else
