@@ -202,31 +202,29 @@ __device__ __forceinline__ int wave_xor_masked(int v) {
 // afterwards, for the winning generator only; ssf_pick_subset).  For every
 // subset size d the minimum residual weight popc(sl ^ M_t) over |t| = d is kept
 // (3 VALU per subset: xor, popcount, min), then score = max_d (popc(sl) -
-// min_d) * 840/d.  Subsets using qubits beyond the generator's weight have zero
-// masks and a larger |t| than the same subset without them, so they never
-// raise the maximum of a positive score.  nhi = 2^(wmax-4) blocks of 16.
+// min_d) * 840/d.  Subsets are visited in Gray-code order, so each one's
+// residual is the previous one's with one qubit mask XORed in (no table of
+// subset masks in registers), and the first 2^w of them are exactly the
+// subsets of the first w qubits.  Subsets using qubits beyond the generator's
+// weight have zero masks and a larger |t| than the same subset without them,
+// so they never raise the maximum of a positive score.  nhi = 2^(wmax-4)
+// blocks of 16.
 __device__ __forceinline__ int gen_best_score(uint32_t sl, const uint32_t (&qm)[kGenW], int nhi) {
     const int base = __builtin_popcount(sl);
-    uint32_t lo[16];
-    lo[0] = 0;
-#pragma unroll
-    for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
     uint32_t mn[kGenW + 1];
 #pragma unroll
     for (int d = 0; d <= kGenW; ++d) mn[d] = 64u;
+    uint32_t r = sl;  // residual of the current Gray-code subset
 #pragma unroll
-    for (int hi = 0; hi < 16; ++hi) {
-        if (hi < nhi) {  // uniform
-            uint32_t mh = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb)
-                if ((hi >> bb) & 1) mh ^= qm[4 + bb];
-            const uint32_t sh = sl ^ mh;
+    for (int blk = 0; blk < 16; ++blk) {
+        if (blk < nhi) {  // uniform
 #pragma unroll
             for (int l = 0; l < 16; ++l) {
-                if (hi == 0 && l == 0) continue;  // empty set
-                const int d = __builtin_popcount(hi) + __builtin_popcount(l);
-                mn[d] = min(mn[d], (uint32_t)__builtin_popcount(sh ^ lo[l]));
+                const int t = blk * 16 + l;
+                if (t == 0) continue;  // empty set
+                r ^= qm[__builtin_ctz(t)];
+                const int d = __builtin_popcount(t ^ (t >> 1));
+                mn[d] = min(mn[d], (uint32_t)__builtin_popcount(r));
             }
         }
     }
@@ -239,39 +237,34 @@ __device__ __forceinline__ int gen_best_score(uint32_t sl, const uint32_t (&qm)[
 // A 1/S share of a generator's subsets (S = 2 or 4), for listing steps with
 // <= 64/S generators: the S lanes l + (64/S) q, q < S, score the same generator,
 // lane q taking the subsets whose top log2(S) qubits (the generator's last ones)
-// are the bits of q.  Per-size minima are then combined by lane-xor shuffles
-// and lane q = 0 gets the same score as gen_best_score (the minima are over the
-// same subsets).  tq = masks of those top qubits (tq[0] the highest),
-// part = nhi / S >= 1 hi values per lane.
+// are the bits of q, the others in Gray-code order over the first qubits.
+// Per-size minima are then combined by lane-xor shuffles and lane q = 0 gets
+// the same score as gen_best_score (the minima are over the same subsets).
+// tq = masks of those top qubits (tq[0] the highest), part = nhi / S >= 1
+// blocks of 16 per lane.
 template <int S>
 __device__ __forceinline__ int gen_best_score_split(uint32_t sl, const uint32_t (&qm)[kGenW], int part,
                                                     const uint32_t (&tq)[2], int q) {
     static_assert(S == 2 || S == 4, "split");
     const int base = __builtin_popcount(sl);
-    uint32_t lo[16];
-    lo[0] = 0;
-#pragma unroll
-    for (int l = 1; l < 16; ++l) lo[l] = lo[l & (l - 1)] ^ qm[__builtin_ctz(l)];
     uint32_t mn[kGenW + 1];
 #pragma unroll
     for (int d = 0; d <= kGenW; ++d) mn[d] = 64u;
     // q's bit 0 selects the highest qubit, bit 1 (S = 4) the next one
     const uint32_t extra = ((q & 1) ? tq[0] : 0u) ^ ((S == 4 && (q & 2)) ? tq[1] : 0u);
+    uint32_t r = sl ^ extra;  // residual of the current subset (top qubits of q included)
+    if (q) mn[0] = (uint32_t)__builtin_popcount(r);  // the top qubits alone (the empty set on q = 0)
 #pragma unroll
-    for (int hh = 0; hh < 8; ++hh) {
-        if (hh < part) {  // uniform
-            uint32_t mh = extra;
-#pragma unroll
-            for (int bb = 0; bb < 3; ++bb)
-                if ((hh >> bb) & 1) mh ^= qm[4 + bb];
-            const uint32_t sh = sl ^ mh;
+    for (int blk = 0; blk < 8; ++blk) {
+        if (blk < part) {  // uniform
 #pragma unroll
             for (int l = 0; l < 16; ++l) {
+                const int t = blk * 16 + l;
+                if (t == 0) continue;
                 // dd = subset size without the top qubits; lane q's size is dd + popc(q)
-                const int dd = __builtin_popcount(hh) + __builtin_popcount(l);
-                uint32_t pc = (uint32_t)__builtin_popcount(sh ^ lo[l]);
-                if (hh == 0 && l == 0) pc = q ? pc : 64u;  // the empty set (lane q = 0 only)
-                mn[dd] = min(mn[dd], pc);
+                r ^= qm[__builtin_ctz(t)];
+                const int dd = __builtin_popcount(t ^ (t >> 1));
+                mn[dd] = min(mn[dd], (uint32_t)__builtin_popcount(r));
             }
         }
     }
