@@ -304,7 +304,10 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 //      (spec: ties -> lowest g, then lowest subset bitmask),
 //   4. the flip updates the residual (u32 per check in LDS) and hard decision.
 // Key (int32): score << 15 | (127 - g) << 8; |score| <= 32*840 < 2^15, g < 128.
-constexpr int kSsfWaves = 4;
+#ifndef QDEC_SSF_WAVES
+#define QDEC_SSF_WAVES 4  // waves per workgroup sharing the generator tables
+#endif
+constexpr int kSsfWaves = QDEC_SSF_WAVES;
 #ifndef QDEC_SSF_INV_INIT
 #define QDEC_SSF_INV_INIT 0  // 1: first-step local syndromes from the inverse table (measured no faster)
 #endif
