@@ -321,6 +321,32 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     wave_lds_sync();
 
     int sb = 0, buf = 0;  // syndrome / readout staging buffers of `shot`
+    // QDEC_DEFER_STORES (LEAN + DEFER, stage depth 1): a shot's per-shot outputs
+    // are stored by the next shot, right after its stage, as exactly kDS store
+    // instructions (null outputs and a shot without them go to a sink in the
+    // handle's control block), so that no wait for a later stage also waits for
+    // these stores to be acknowledged; the waits below count them
+    constexpr bool DS = QDEC_DEFER_STORES && LEAN && DEFER && Io::kDepth == 1;
+    constexpr int kDS = DS ? 4 : 0;
+    int64_t p_shot = -1;     // shot whose outputs are pending (-1: none)
+    int p_iters = 0, p_fin = 0, p_fail = 0, p_status = 0;  // p_fin: status / steps / fail pending too
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(a.wave_ctr) + 128;
+    auto flush = [&]() {
+        if constexpr (DS) {
+            const bool v = p_shot >= 0, f = v && p_fin;
+            int32_t* pi = (v && a.iters) ? a.iters + p_shot : reinterpret_cast<int32_t*>(sink);
+            uint8_t* ps = (f && a.status) ? a.status + p_shot : sink + 4;
+            int32_t* pq = (f && a.ssf_steps) ? a.ssf_steps + p_shot : reinterpret_cast<int32_t*>(sink + 8);
+            uint8_t* pf = (f && a.fail) ? a.fail + p_shot : sink + 12;
+            if (lane == 0) {
+                __builtin_nontemporal_store(p_iters, pi);
+                __builtin_nontemporal_store((uint8_t)p_status, ps);
+                __builtin_nontemporal_store(0, pq);
+                __builtin_nontemporal_store((uint8_t)p_fail, pf);
+            }
+        }
+    };
+    flush();  // sink stores: the waits below count kDS stores after every stage, from the first
     QDEC_STAMP_DECL
 #ifdef QDEC_STAMPS
     const unsigned long long qdec_t0 = __builtin_amdgcn_s_memtime(), qdec_r0 = __builtin_amdgcn_s_memrealtime();
@@ -330,7 +356,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         // of the same stage and the later stages are younger); then stage the
         // shot kDepth ahead ----
         QDEC_STAMP(5);
-        wait_vmem<Io::kWaitSyn>();
+        wait_vmem<Io::kWaitSyn + kDS>();
         Io::patch_tail(a.syn, a.B, m, shot, io.syn_area(sb), sh.s, lane);
         wave_lds_sync();
         QDEC_STAMP(0);
@@ -345,6 +371,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         const int64_t nn = seq.next(lane);  // any counter request is older than the stage
         const typename Io::Shift shn = Io::kDepth == 2 ? io.stage(g, a, nxt2, sb, buf == 0 ? 2 : buf - 1, lane)
                                                        : io.stage(g, a, nxt, 0, buf ^ 1, lane);
+        flush();  // the previous shot's outputs (DS), after the stage
         if (!LEAN && a.syn_flags) {
             const bool use_b = (a.syn_flags & 1) && a.base;
             const bool use_r = (a.syn_flags & 2) && a.readout;
@@ -581,10 +608,16 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         // kWaitRd most recent vector-memory operations are the later shots' stages
         const bool need_rd = a.readout && a.fail && g.k > 0;  // the SSF queue carries it too
         if (need_rd) {
-            wait_vmem<Io::kWaitRd>();
+            wait_vmem<Io::kWaitRd + 2 * kDS>();
             Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd_area(buf), sh.r, lane);
         }
-        if (lane == 0 && a.iters) a.iters[shot] = iters;
+        if constexpr (DS) {
+            p_shot = shot;
+            p_iters = iters;
+            p_fin = 0;
+        } else if (lane == 0 && a.iters) {
+            a.iters[shot] = iters;
+        }
         // hard decision by column (slot order -> xh[column])
 #pragma unroll
         for (int rv = 0; rv < RV; ++rv) xh[col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
@@ -633,7 +666,11 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
                 for (int w = 0; w < RV; ++w) Xc[w] = __ballot(xh[w * 64 + lane] & 1);
                 any_fail = fail_from_words<RV, !LEAN>(g, a, shot, lane, Xc, io.rd_area(buf) + sh.r, io.lz);
             }
-            if (lane == 0) {
+            if constexpr (DS) {
+                p_fin = 1;
+                p_status = conv ? 3 : 0;
+                p_fail = any_fail;
+            } else if (lane == 0) {
                 if (a.status) a.status[shot] = (uint8_t)(conv ? 3 : 0);
                 if (a.ssf_steps) a.ssf_steps[shot] = 0;
                 if (a.fail) a.fail[shot] = (uint8_t)any_fail;
@@ -662,6 +699,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     QDEC_COUNT(11, __builtin_amdgcn_s_memrealtime() - qdec_r0);
     QDEC_COUNT(12, 1);
 #endif
+    flush();  // the last shot's outputs
     QDEC_FLUSH_AT(0);
 }
 

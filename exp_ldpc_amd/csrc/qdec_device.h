@@ -386,6 +386,9 @@ __device__ __forceinline__ int lz_row_parity(const DevGraph& g, const uint64_t* 
     return par & 1;
 }
 
+#ifndef QDEC_DEFER_STORES
+#define QDEC_DEFER_STORES 0
+#endif
 #ifndef QDEC_STAGE_DEPTH
 #define QDEC_STAGE_DEPTH 1
 #endif

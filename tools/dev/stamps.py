@@ -15,7 +15,7 @@ B = 1 << 18
 dev = torch.device("cuda", 0)
 names = ["wait_syn", "stage+init", "iterations", "post", "finalize", "loop_top"]
 for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
-    dec = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, flip_sets=hx, logicals=lz)
+    dec = Decoder(hz, 2 * p / 3, method="ms", precision=os.environ.get("STAMP_PREC", "f32"), max_iter=50, flip_sets=hx, logicals=lz)
     syn = torch.empty((B, 108), dtype=torch.uint8, device=dev)
     rd = torch.empty((B, 225), dtype=torch.uint8, device=dev)
     dec.sample_storage_device(0, p, p, 1, 0, 0, B, syn, rd)
@@ -40,7 +40,7 @@ for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
 
 # SSF kernel phases (slots 16..31)
 for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
-    dec = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, flip_sets=hx, logicals=lz)
+    dec = Decoder(hz, 2 * p / 3, method="ms", precision=os.environ.get("STAMP_PREC", "f32"), max_iter=50, flip_sets=hx, logicals=lz)
     syn = torch.empty((B, 108), dtype=torch.uint8, device=dev)
     rd = torch.empty((B, 225), dtype=torch.uint8, device=dev)
     dec.sample_storage_device(0, p, p, 1, 0, 0, B, syn, rd)
