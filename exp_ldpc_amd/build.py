@@ -45,7 +45,8 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False, defines=(), tag: str = "") -> str:
+def build(force: bool = False, verbose: bool = False, stamps: bool = False, defines=(), tag: str = "",
+          flags=()) -> str:
     """Build the library; stamps=True builds the development variant with phase
     timers (libqdec_hip_stamps.so), `defines` + `tag` a development variant
     (libqdec_hip_<tag>.so); variants are loaded with QDEC_LIB=....  Every source
@@ -56,7 +57,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
     lib = LIB.replace(".so", suffix + ".so")
     if not force and not suffix and not _stale():
         return LIB
-    extra = (["-DQDEC_STAMPS"] if stamps else []) + [f"-D{d}" for d in defines]
+    extra = (["-DQDEC_STAMPS"] if stamps else []) + [f"-D{d}" for d in defines] + list(flags)
     objdir = os.path.join(os.path.dirname(HERE), "build", "obj" + suffix)
     os.makedirs(objdir, exist_ok=True)
     cflags = [f for f in FLAGS if f != "-shared"]
