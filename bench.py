@@ -38,15 +38,21 @@ process before anything touches the GPU and exits with its status.  Shots are
 sharded by index (rank r decodes shot range (step*N + r)*B ..), no data-path
 collective; a barrier + synchronize brackets the timed region and rank 0
 reports the max time over ranks.  value = shots decoded by all ranks / time.
+The bookkeeping (barrier, max time, summed failure counts) runs on host words
+over a gloo group (exp_ldpc_amd/sharding.py) on the GPU path and in the CPU
+rehearsal alike; rank r uses HIP device r mod (visible devices), so N ranks
+can also be rehearsed on one GPU.
 
-Roofline (dominant kernel = the f64 BP kernel): `achieved` = algorithmic HBM
-bytes per launch (the compulsory per-shot I/O, 339 B: 108 B syndrome + 225 B
-readout in, fail + status + 4-B iteration count out) / the kernel's isolated
-average launch time.  BP messages live in LDS/registers at n = 225 and never
-touch HBM, so this fraction is small by construction; the ceilings that bind
-(VALU issue, LDS) come from the committed PMC summary of this same command
-(profiles/*_pmc_summary.json; tools/pmc.sh + tools/pmc_summary.py), as does
-`traffic` (HBM bytes per launch, FETCH_SIZE x2 + WRITE_SIZE).
+Roofline (dominant kernel = the f64 BP kernel, named exactly as it ran by
+Decoder.last_kernels()): its messages never leave the CU at n = 225, so
+`bound` is "lds": `achieved` = algorithmic LDS bytes of the isolated launches
+(32 B per edge + 16 B per check per BP iteration, times the launches' own
+iteration totals) / their HIP-event durations, against the LDS's aggregate
+peak.  The compulsory-HBM line (339 B of I/O per shot) sits beside it under
+`roofline.hbm` and per sweep point under `roofline.per_point`; the PMC figures
+of the same instantiation (profiles/*_pmc_summary.json; tools/pmc.sh +
+tools/pmc_summary.py) give `ceilings` and `traffic` (HBM bytes per launch,
+FETCH_SIZE x2 + WRITE_SIZE).
 """
 from __future__ import annotations
 
@@ -65,10 +71,13 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+from exp_ldpc_amd.sharding import barrier, max_time, reduce_counts  # noqa: E402  (pure Python, no GPU)
+
 METRIC = "decoded syndrome shots/sec + logical error rate, (3,4)-HGP n=225 @ 1/2/4/8 GPUs"
 CODE = "hgp_12_3_4_s1234"
 SEED = 20250221
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b64/b128 rate, every CU streaming (MI355X_MICROARCH.md §LDS)
 IO_BYTES_PER_SHOT = 108 + 225 + 1 + 1 + 4  # syndrome + readout in; fail, status, iters out
 
 
@@ -92,10 +101,14 @@ def load_code():
         return read_quantum_code(f, validate_stabilizer_code=True)
 
 
-def pmc_ceilings(kernel_prefix: str):
-    """Per-launch PMC figures of the BP kernel from the newest committed PMC
-    summary (profiles/*_pmc_summary.json, written by tools/pmc_summary.py from
-    a rocprofv3 --pmc run of this bench command), or None."""
+def pmc_ceilings(kernel: str):
+    """Per-launch PMC figures of exactly `kernel` (rocprof's spelling with its
+    template arguments, as Decoder.last_kernels() reports it) from the newest
+    committed PMC summary that holds it (profiles/*_pmc_summary.json, written by
+    tools/pmc_summary.py from rocprofv3 --pmc passes of this bench command), or
+    None."""
+    if not kernel:
+        return None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
     for f in reversed(files):
         try:
@@ -104,9 +117,48 @@ def pmc_ceilings(kernel_prefix: str):
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if name.startswith(kernel_prefix) and "derived" in k:
+            if name.split("(", 1)[0] == kernel and "derived" in k:
                 return os.path.relpath(f, REPO), name, k
     return None
+
+
+def lds_roofline(bp_ms, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms):
+    """Roofline of the dominant kernel, the BP kernel at n = 225: its messages
+    never leave the CU, so the unit that bounds it is the LDS.  achieved =
+    algorithmic LDS bytes of the isolated launches (per shot-iteration: every
+    edge's v2c message read by its check (8 B) and written back by its variable
+    (8 B), every edge's (m1, m2) check state gathered by its variable (16 B),
+    every check's state written (16 B); counted from the launches' own
+    iteration totals) / their HIP-event durations; peak = the LDS's aggregate
+    rate with every CU streaming (MI355X_MICROARCH.md §LDS: ~150 TB/s for
+    ds_read_b64/b128).  The HBM line (compulsory I/O per shot) is kept beside
+    it, per launch and per sweep point."""
+    E, m = int(hz.nnz), int(hz.shape[0])
+    lds_per_it = 32 * E + 16 * m
+    tot_ms = float(bp_ms.sum())
+    lds_bytes = float(lds_per_it * it_iso.sum())
+    achieved = lds_bytes / (tot_ms * 1e-3) / 1e9
+    io_launch = IO_BYTES_PER_SHOT * args.batch
+    hbm_ach = io_launch / (bp_ms.mean() * 1e-3) / 1e9
+    per_point = {}
+    for pi in range(bp_ms.shape[1]):
+        ms = float(bp_ms[:, pi].mean())
+        per_point[str(pi)] = {"bp_ms": ms, "hbm_frac": io_launch / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "lds_frac": lds_per_it * float(it_iso[:, pi].mean()) / (ms * 1e-3) / 1e9 / LDS_PEAK_GBS}
+    return {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": achieved / LDS_PEAK_GBS,
+            "traffic": None, "kernel": bp_kernel, "avg_launch_ms": float(bp_ms.mean()), "launches": int(bp_ms.size),
+            "timing": "HIP events recorded by the library on the launch stream around each kernel, isolated phase "
+                      "(one stream)",
+            "algorithmic_bytes_per_launch": lds_bytes / bp_ms.size,
+            "bytes_model": f"LDS: 32 B per edge + 16 B per check per BP iteration ({lds_per_it} B per shot-iteration "
+                           f"at E={E}, m={m}) x the launch's summed iterations",
+            "hbm": {"achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
+                    "algorithmic_bytes_per_launch": io_launch,
+                    "bytes_model": f"per shot {IO_BYTES_PER_SHOT} B compulsory HBM I/O (108 B syndrome + 225 B "
+                                   "readout in, fail + status + int32 iterations out)"},
+            "per_point": per_point,
+            "ssf_kernel": ssf_kernel, "ssf_avg_launch_ms": float(ssf_ms.mean()),
+            "isolated_step_ms": float(bp_ms.sum(axis=1).mean() + ssf_ms.sum(axis=1).mean())}
 
 
 def launch_children(args) -> int:
@@ -303,9 +355,7 @@ class Run:
             self.torch.cuda.synchronize(self.dev)
 
     def barrier(self):
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.barrier()
+        barrier()  # sharding: CPU word over the gloo bookkeeping group
 
     def pipelined(self, decs, on: bool):
         """Route (or stop routing) the decoders' SSF kernels to the SSF stream."""
@@ -365,27 +415,17 @@ class Run:
             self.step(decs, s, streams)
         self.sync()
         self.barrier()
-        elapsed = time.perf_counter() - t0
-        if self.world > 1:
-            import torch.distributed as dist
-            tt = self.torch.tensor([elapsed], dtype=self.torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
-        return elapsed
+        return max_time(time.perf_counter() - t0)
 
     def counts(self):
         """Failures / BP-converged per point over the timed steps, summed over ranks."""
         torch = self.torch
         w = self.args.warmup
-        fails = self.fail[w:].to(torch.int64).sum(dim=(0, 2)).cpu()
-        conv = (self.status[w:] & 1).to(torch.int64).sum(dim=(0, 2)).cpu()
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(fails)
-            dist.all_reduce(conv)
+        fails = np.array(reduce_counts(self.fail[w:].to(torch.int64).sum(dim=(0, 2))))
+        conv = np.array(reduce_counts((self.status[w:] & 1).to(torch.int64).sum(dim=(0, 2))))
         itp = self.iters[w:].to(torch.float64).mean(dim=(0, 2)).cpu().numpy()
         ssp = self.ssf_steps[w:].to(torch.float64).mean(dim=(0, 2)).cpu().numpy()
-        return fails.numpy(), conv.numpy(), itp, ssp
+        return fails, conv, itp, ssp
 
 
 def main():
@@ -429,18 +469,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
-    import torch.distributed as dist
+    from exp_ldpc_amd.sharding import init_process_group, rank_device
 
     fake = args.fake_device
+    if world > 1:  # the same gloo bookkeeping group on the GPU path and the CPU rehearsal
+        init_process_group()
     if fake:
         dev = torch.device("cpu")
-        if world > 1:
-            dist.init_process_group("gloo")
     else:
+        local = rank_device(local, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
 
     code = load_code()
     hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
@@ -511,7 +550,8 @@ def main():
             bp_ms[:, pi] = a[:args.iso_steps]
             ssf_ms[:, pi] = c[:args.iso_steps]
         it_iso = run.iters[args.warmup:args.warmup + args.iso_steps].to(torch.int64).sum(dim=2).cpu().numpy()
-        iso[prec] = (bp_ms, ssf_ms, it_iso)
+        names = ("", "") if fake else dset[-1].last_kernels()  # the instantiations the isolated phase ran
+        iso[prec] = (bp_ms, ssf_ms, it_iso, names)
 
     # ---- phase 4: sampling + decode in the timed region ----
     sd = None
@@ -553,26 +593,9 @@ def main():
                 row[variant[0]] = vr
             ler[key] = row
 
-        bp_ms, ssf_ms, it_iso = iso[args.precision]
-        bytes_per_launch = IO_BYTES_PER_SHOT * args.batch
-        achieved = bytes_per_launch / (bp_ms.mean() * 1e-3) / 1e9
-        kname = "qdec::bp_ms_wave_kernel<" + ("double" if args.precision == "f64" else "float")
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": kname + ", 2, 4, 7, true, true, 2, 0> (BP min-sum, lean outputs, queues BP failures; the "
-                          "overlapped phases run its 3-waves-per-SIMD build <..., 2, 3>)",
-                "avg_launch_ms": float(bp_ms.mean()), "launches": int(bp_ms.size),
-                "timing": "HIP events recorded by the library on the launch stream around each kernel, "
-                          "isolated phase (one stream)",
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "bytes_model": f"per shot {IO_BYTES_PER_SHOT} B compulsory HBM I/O (108 B syndrome + 225 B readout in, "
-                               "fail + status + int32 iterations out); BP messages stay on chip",
-                "ssf_kernel": "qdec::ssf_wave_kernel<2, 4, 2>", "ssf_avg_launch_ms": float(ssf_ms.mean()),
-                "isolated_step_ms": float(bp_ms.sum(axis=1).mean() + ssf_ms.sum(axis=1).mean()),
-                "message_model": {"bytes_per_launch": float(16 * int(hz.nnz) * it_iso.mean()),
-                                  "note": "SURVEY §8(d): 16 B per edge per BP iteration; on-chip LDS/register "
-                                          "traffic at n=225, not HBM"}}
-        pmc = None if fake else pmc_ceilings(kname)
+        bp_ms, ssf_ms, it_iso, (bp_kernel, ssf_kernel) = iso[args.precision]
+        roof = lds_roofline(bp_ms, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms)
+        pmc = None if fake else pmc_ceilings(bp_kernel)
         if pmc is not None:
             src, name, k = pmc
             dv = k["derived"]
@@ -581,28 +604,15 @@ def main():
                                 **{key: dv.get(key) for key in ("valu_issue_frac", "lds_frac",
                                                                 "lds_bank_conflict_ratio", "hbm_frac", "clock_ghz",
                                                                 "duration_ms", "formulas")}}
-            # the binding on-chip ceiling: HBM is `bound` by the §8(d) contract,
-            # but the kernel's messages never leave LDS / registers, so what
-            # limits it is the busier of the LDS array and the VALU issue
-            lf, vf = dv.get("lds_frac"), dv.get("valu_issue_frac")
-            if lf is not None and vf is not None:
-                roof["on_chip_bound"] = {
-                    "unit": "lds" if lf >= vf else "valu", "lds_busy": lf, "valu_issue": vf,
-                    "lds_bank_conflict_ratio": dv.get("lds_bank_conflict_ratio"),
-                    "note": "per-wave LDS work per BP iteration (f64): 6 ds_read_b128 + 2 ds_read_b64 row reads, "
-                            "2 ds_write_b128 state writes, 14 ds_read_b128 state gathers, 14 ds_write_b64 v2c "
-                            "scatters = 211 LDS-array cycles with bank conflicts by the layout model "
-                            "(tools/dev/ms_conflicts.py; PMC of the previous layout: 225, model 231); valu_issue "
-                            "prices every wave64 VALU op at 2 cycles, the loop's f64 ops take ~4.9 (98 of them per "
-                            "iteration since the sign-bit check pass, 124 before; DESIGN.md §3.1, §4); HBM frac "
-                            "above is compulsory I/O"}
+            lf = dv.get("lds_frac")
+            if lf is not None:
+                roof["lds_busy_pmc"] = lf
         calib = os.path.join(REPO, "profiles", "r03_hbm_calibration")
         if os.path.isdir(calib):
-            roof["traffic_calibration"] = {
+            roof["hbm"]["traffic_calibration"] = {
                 "source": os.path.relpath(calib, REPO),
                 "note": "FETCH_SIZE of this kernel equals that of a staging-only build with the BP loop compiled "
-                        "out (QDEC_CALIB_NOBP): the messages add no HBM bytes; traffic above the compulsory I/O is "
-                        "the LDS-DMA row staging (whole 256-B dword blocks per row) and 1-4 B scattered outputs"}
+                        "out (QDEC_CALIB_NOBP): the messages add no HBM bytes"}
 
         result = {
             "metric": METRIC, "value": value, "unit": "shots/s", "n_gpus": world, "steps": args.steps,
@@ -619,7 +629,7 @@ def main():
                        "wave_waves_per_cu": {k: (v or "default") for k, v in occ.items()}},
         }
         if variant:
-            vb, vs, _ = iso[variant[0]]
+            vb, vs, _, _ = iso[variant[0]]
             result["variants"] = [{"dtype": variant[0], "value": total_shots / variant[1],
                                    "ms_per_step": variant[1] / args.steps * 1e3,
                                    "bp_kernel_ms_isolated_avg": float(vb.mean()),
@@ -640,6 +650,7 @@ def main():
                 "variant_vs_cpu_f64": all(r[variant[0]]["overlaps_cpu_f64"] for r in ler.values()) if variant else None}
         print(json.dumps(result))
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -45,8 +45,16 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+# host-only ASan + UBSan variant (tools/sanitize.sh): every -fsanitize=
+# applies to the host compilation only (-Xarch_host), the device code is the
+# product's; the runtime comes from the process (LD_PRELOAD of clang's libasan)
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-g"]
+SAN_LINK = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-shared-libsan"]
+
+
 def build(force: bool = False, verbose: bool = False, stamps: bool = False, defines=(), tag: str = "",
-          flags=()) -> str:
+          flags=(), link_flags=()) -> str:
     """Build the library; stamps=True builds the development variant with phase
     timers (libqdec_hip_stamps.so), `defines` + `tag` a development variant
     (libqdec_hip_<tag>.so); variants are loaded with QDEC_LIB=....  Every source
@@ -78,7 +86,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = lib + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", tmp, *objs]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *link_flags, "-o", tmp, *objs]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-6000:]}")
@@ -87,8 +95,10 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
 
 
 if __name__ == "__main__":
-    # python -m exp_ldpc_amd.build [--force] [--stamps] [--tag T -DNAME=V ...]
+    # python -m exp_ldpc_amd.build [--force] [--stamps] [--san] [--tag T -DNAME=V ...]
     argv = sys.argv[1:]
     tag = argv[argv.index("--tag") + 1] if "--tag" in argv else ""
     defs = [a[2:] for a in argv if a.startswith("-D")]
-    print(build(force="--force" in argv, verbose=True, stamps="--stamps" in argv, defines=defs, tag=tag))
+    san = "--san" in argv
+    print(build(force="--force" in argv, verbose=True, stamps="--stamps" in argv, defines=defs, tag=tag,
+                flags=SAN_FLAGS if san else (), link_flags=SAN_LINK if san else ()))

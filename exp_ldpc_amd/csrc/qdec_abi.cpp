@@ -50,13 +50,22 @@ int guarded(F&& f) {
     }
 }
 
-// A device allocation list owned by the graph.
+// A device allocation list owned by the graph.  A host-only arena
+// (qd_graph_create_host: table builds without a GPU, for tests and sanitizer
+// runs) keeps host copies instead and makes no HIP call.
 struct DevArena {
     std::vector<void*> ptrs;
+    bool host = false;
+    std::vector<std::vector<uint8_t>> kept;  // host-only: the uploaded bytes, in order
     template <typename T>
     const T* upload(const std::vector<T>& h) {
-        void* d = nullptr;
         const size_t bytes = std::max<size_t>(h.size() * sizeof(T), 16);
+        if (host) {
+            kept.emplace_back(bytes, 0);
+            if (!h.empty()) std::memcpy(kept.back().data(), h.data(), h.size() * sizeof(T));
+            return reinterpret_cast<const T*>(kept.back().data());
+        }
+        void* d = nullptr;
         hip_check(hipMalloc(&d, bytes), "hipMalloc");
         ptrs.push_back(d);
         if (!h.empty()) hip_check(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy H2D");
@@ -65,6 +74,7 @@ struct DevArena {
     void release() {
         for (void* p : ptrs) (void)hipFree(p);
         ptrs.clear();
+        kept.clear();
     }
 };
 
@@ -108,6 +118,10 @@ struct qd_graph {
     hipStream_t ssf_stream = nullptr;
     hipEvent_t ssf_ev = nullptr;
     hipStream_t ws_last = nullptr;
+    // kernels the last decode on this handle launched (qd_graph_last_kernels)
+    std::string last_bp, last_ssf;
+    // qd_graph_create_host: tables only, no device, no stream; decodes refuse it
+    bool host_only = false;
 };
 
 namespace {
@@ -117,7 +131,9 @@ int drs() { return lds_stride<T, kDR>(); }
 template <typename T>
 int dcs() { return lds_stride<T, kDC>(); }
 
-void set_device(qd_graph* g) { hip_check(hipSetDevice(g->device), "hipSetDevice"); }
+void set_device(qd_graph* g) {
+    if (!g->host_only) hip_check(hipSetDevice(g->device), "hipSetDevice");
+}
 
 // Workspace chain (see qd_graph::ws_ev).
 void ws_acquire(qd_graph* G, hipStream_t s) {
@@ -683,7 +699,7 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
 }
 
 void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& a, size_t* bytes) {
-    const size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus, a);
+    size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus, a);
     *bytes = need;
     if (need == 0) return nullptr;
     if (need > G->mws_bytes) {
@@ -691,10 +707,28 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
         if (G->mws) hip_check(hipFree(G->mws), "hipFree scratch");
         G->mws = nullptr;
         G->mws_bytes = 0;
-        hip_check(hipMalloc(&G->mws, need), "hipMalloc message scratch");
+        // on an allocation failure, halve the slot groups in flight down to one
+        // (the launch sizes its grid from the bytes it gets; results do not change)
+        const size_t floor = block_scratch_floor(G->dg, method, precision, G->num_cus, a);
+        for (;;) {
+            const hipError_t e = hipMalloc(&G->mws, need);
+            if (e == hipSuccess) break;
+            (void)hipGetLastError();  // clear the sticky error before any launch checks it
+            G->mws = nullptr;
+            if (e != hipErrorOutOfMemory || need <= floor)
+                hip_check(e, "hipMalloc message scratch");
+            need = std::max(floor, floor + (need - floor) / 2);
+        }
         G->mws_bytes = need;
+        *bytes = need;
     }
     return G->mws;
+}
+
+void note_kernels(qd_graph* G) {
+    const LaunchNames& n = last_launch_names();
+    G->last_bp = n.bp ? n.bp : "";
+    G->last_ssf = n.ssf ? n.ssf : "";
 }
 
 void attach_timing(qd_graph* G, DecodeArgs& a) {
@@ -713,6 +747,7 @@ void check_graph(const qd_graph* g) {
 }
 
 void check_params(const qd_graph* g, const qd_params* p) {
+    if (g->host_only) throw Fail(-16, "host-only graph (qd_graph_create_host): no device to decode on");
     if (!p) throw Fail(-2, "null params");
     if (p->method != QD_MIN_SUM && p->method != QD_PRODUCT_SUM) throw Fail(-3, "unknown BP method");
     if (p->precision != QD_F32 && p->precision != QD_F64) throw Fail(-4, "unknown precision");
@@ -813,9 +848,73 @@ int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t*
     });
 }
 
+int qd_graph_create_host(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx, int32_t n_data,
+                         int32_t fold_blocks, qd_graph** out) {
+    return guarded([&] {
+        if (!out) throw Fail(-1, "null output handle");
+        *out = nullptr;
+        if (m <= 0 || n <= 0 || !row_ptr || !col_idx) throw Fail(-10, "invalid graph shape or null arrays");
+        if (n_data <= 0 || fold_blocks <= 0 || (int64_t)n_data * fold_blocks > n)
+            throw Fail(-11, "invalid fold (n_data * fold_blocks must be <= n)");
+        if (row_ptr[0] != 0) throw Fail(-12, "row_ptr[0] must be 0");
+        for (int i = 0; i < m; ++i) {
+            if (row_ptr[i + 1] < row_ptr[i]) throw Fail(-12, "row_ptr not monotone");
+            for (int e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+                if (col_idx[e] < 0 || col_idx[e] >= n) throw Fail(-13, "column index out of range");
+                if (e > row_ptr[i] && col_idx[e] <= col_idx[e - 1])
+                    throw Fail(-14, "column indices must be strictly ascending within a row");
+            }
+        }
+        auto* G = new qd_graph();
+        G->host_only = true;
+        for (DevArena* a : {&G->arena, &G->flip_arena, &G->lz_arena, &G->prior_arena}) a->host = true;
+        G->num_cus = 256;
+        try {
+            G->row_ptr.assign(row_ptr, row_ptr + m + 1);
+            G->col_idx.assign(col_idx, col_idx + row_ptr[m]);
+            G->dg.n_data = n_data;
+            G->dg.fold_blocks = fold_blocks;
+            build_tables(G, m, n);
+            G->dg.lz_words = (n_data + 63) / 64;
+            G->dg.k = 0;
+            G->dg.lz = nullptr;
+            G->dg.lz_ptr = G->dg.lz_idx = nullptr;
+            G->dg.lz_sparse = 0;
+            G->dg.n_gen = 0;
+            G->dg.g_inv = nullptr;
+            G->dg.g_invd = G->dg.g_invl = 0;
+        } catch (...) {
+            delete G;
+            throw;
+        }
+        *out = G;
+    });
+}
+
+int qd_graph_table_digest(const qd_graph* G, uint64_t* digest, int64_t* bytes) {
+    return guarded([&] {
+        check_graph(G);
+        if (!G->host_only) throw Fail(-16, "table digests are kept for host-only graphs (qd_graph_create_host)");
+        uint64_t h = 1469598103934665603ull;  // FNV-1a over every table, in upload order
+        int64_t total = 0;
+        for (const DevArena* a : {&G->arena, &G->flip_arena, &G->lz_arena, &G->prior_arena})
+            for (const auto& v : a->kept) {
+                for (uint8_t b : v) h = (h ^ b) * 1099511628211ull;
+                total += (int64_t)v.size();
+            }
+        if (digest) *digest = h;
+        if (bytes) *bytes = total;
+    });
+}
+
 int qd_graph_destroy(qd_graph* g) {
     return guarded([&] {
         if (!g) return;
+        if (g->host_only) {
+            for (DevArena* a : {&g->arena, &g->flip_arena, &g->lz_arena, &g->prior_arena}) a->release();
+            delete g;
+            return;
+        }
         (void)hipSetDevice(g->device);
         if (g->stream) (void)hipStreamSynchronize(g->stream);
         if (g->ws_ev_live) (void)hipEventSynchronize(g->ws_ev);
@@ -1094,6 +1193,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         }
         ws_acquire(G, s);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
+        note_kernels(G);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         // the last user of the queue is the SSF kernel: the workspace chain
         // continues on its stream (the next decode on this handle waits for it)
@@ -1152,6 +1252,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         void* scr = message_scratch(G, p->method, p->precision, a, &sb);
         ws_acquire(G, s);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
+        note_kernels(G);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         ws_release(G, s);
         auto d2h = [&](void* h, const Reg& r, const char* what) {
@@ -1279,6 +1380,20 @@ int qd_graph_read_timing(qd_graph* G, float* bp_ms, float* ssf_ms, int32_t max_c
         }
         *n_calls = n;
         G->t_count = 0;
+    });
+}
+
+int qd_graph_last_kernels(qd_graph* G, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len) {
+    return guarded([&] {
+        check_graph(G);
+        auto put = [](const std::string& v, char* out, int32_t len) {
+            if (!out || len <= 0) return;
+            const size_t k = std::min(v.size(), (size_t)len - 1);
+            std::memcpy(out, v.data(), k);
+            out[k] = '\0';
+        };
+        put(G->last_bp, bp, bp_len);
+        put(G->last_ssf, ssf, ssf_len);
     });
 }
 

@@ -668,6 +668,11 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
 }
 
 // ---------------------------------------------------------------- launcher
+LaunchNames& last_launch_names() {
+    static thread_local LaunchNames n;
+    return n;
+}
+
 template <typename T>
 static size_t wave_lds_bytes(const DevGraph& g) {
     constexpr int DRS = lds_stride<T, kDR>();
@@ -678,6 +683,8 @@ static size_t wave_lds_bytes(const DevGraph& g) {
 
 template <int RG, int XW, int RW>
 static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    // the fused failure check reads the dense logical table's LDS copy (as launch_bp_wave)
+    if (a.fail && g.k > 0 && !g.lz) return (int)hipErrorInvalidValue;
     const size_t lds = SsfLds<RG>::shared_bytes(g) + kSsfWaves * SsfLds<RG>::wave_bytes(g);
     if (lds > 64 * 1024) {
         const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ssf_wave_kernel<RG, XW, RW>),
@@ -693,6 +700,7 @@ static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, 
     const long long need = (a.B + kSsfWaves - 1) / kSsfWaves;  // queue length <= B
     if (grid > need) grid = need;
     if (grid <= 0) return 0;
+    QDEC_NOTE_SSF("qdec::ssf_wave_kernel", RG, XW, RW);
     hipLaunchKernelGGL((ssf_wave_kernel<RG, XW, RW>), dim3((unsigned)grid), dim3(64 * kSsfWaves), lds, stream, g, a);
     return (int)hipGetLastError();
 }
@@ -748,24 +756,33 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
             if (g.ms_d3r >= 2) {
                 if constexpr (sizeof(T) == 8) {
-                    if (lean && cap > 8)  // 3 waves per SIMD: the 168-VGPR build
+                    if (lean && cap > 8) {  // 3 waves per SIMD: the 168-VGPR build
+                        QDEC_NOTE_BP("qdec::bp_ms_wave_kernel", tname<T>(), RC, RV, DRC, DEFER, true, 2, 3);
                         return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 2, 3>, lds, a.B,
                                                  num_cus, stream, g, a, 64, cap);
+                    }
                 }
-                if (lean)
+                if (lean) {
+                    QDEC_NOTE_BP("qdec::bp_ms_wave_kernel", tname<T>(), RC, RV, DRC, DEFER, true, 2, 0);
                     return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 2>, lds, a.B, num_cus,
                                              stream, g, a, 64, cap);
+                }
+                QDEC_NOTE_BP("qdec::bp_ms_wave_kernel", tname<T>(), RC, RV, DRC, DEFER, false, 2, 0);
                 return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 2>, lds, a.B, num_cus,
                                          stream, g, a, 64, cap);
             }
         }
-        if (lean)
+        if (lean) {
+            QDEC_NOTE_BP("qdec::bp_ms_wave_kernel", tname<T>(), RC, RV, DRC, DEFER, true, 0, 0);
             return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, true, 0>, lds, a.B, num_cus, stream, g, a,
                                      64, cap);
+        }
+        QDEC_NOTE_BP("qdec::bp_ms_wave_kernel", tname<T>(), RC, RV, DRC, DEFER, false, 0, 0);
         return launch_persistent(bp_ms_wave_kernel<T, RC, RV, DRC, DEFER, false, 0>, lds, a.B, num_cus, stream, g, a,
                                  64, cap);
     } else {
         const size_t lds = (wave_lds_bytes<T>(g) + 15) / 16 * 16;
+        QDEC_NOTE_BP("qdec::bp_wave_kernel", tname<T>(), METHOD, RC, RV, DRC, DEFER);
         return launch_persistent(bp_wave_kernel<T, METHOD, RC, RV, DRC, DEFER>, lds, a.B, num_cus, stream, g, a);
     }
 }
@@ -831,6 +848,7 @@ bool wave_kernel_supports(const DevGraph& g) {
 
 int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
                   hipStream_t stream, void* scratch, size_t scratch_bytes) {
+    last_launch_names() = LaunchNames{};
     if (a.B <= 0) return 0;
     if (!g.wave || !wave_kernel_supports(g))
         return launch_decode_block(g, method, precision, a, num_cus, stream, scratch, scratch_bytes);

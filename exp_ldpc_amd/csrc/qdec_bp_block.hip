@@ -1444,6 +1444,7 @@ static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus,
     e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);  // shot counter
     if (e != hipSuccess) return (int)e;
     record_ev(a, 0, stream);
+    QDEC_NOTE_BP("qdec::bp_ms_lds_kernel", VPT);
     hipLaunchKernelGGL((bp_ms_lds_kernel<VPT>), dim3((unsigned)grid), dim3(kMlThreads), lds, stream, g, a, g.ml_etab,
                        reinterpret_cast<const float*>(g.prior[1][1]));
     const hipError_t le = hipGetLastError();
@@ -1467,19 +1468,51 @@ static int launch_lds(const DevGraph& g, const DecodeArgs& a, int num_cus, hipSt
 }
 
 // ---------------------------------------------------------------- slot-group launch
+// HBM budget of one handle's group scratch: QDEC_GROUP_SCRATCH_MB when set, else
+// a quarter of the device memory free right now (a bpssf_hybrid pipeline holds
+// two such handles; the batch cap in group_count keeps small decodes small)
 static size_t group_scratch_budget() {
-    const char* v = getenv("QDEC_GROUP_SCRATCH_MB");
-    const long long mb = v ? atoll(v) : 98304;  // 96 GiB of the 288 GB HBM
-    return (size_t)std::max(64ll, mb) << 20;
+    if (const char* v = getenv("QDEC_GROUP_SCRATCH_MB")) return (size_t)std::max(64ll, atoll(v)) << 20;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)4 << 30;
+    return std::max<size_t>(free_b / 4, (size_t)64 << 20);
 }
 
-// Groups in flight: as many per CU as the occupancy allows, capped by the
-// scratch budget and by the batch (every slot should see >= 2 shots, so the
-// tail of a launch stays short and small test batches stay small).
-static int64_t group_count(const DevGraph& g, size_t tsz, int num_cus, int64_t B) {
+template <typename T, int METHOD, int DR, int DC>
+static int group_occupancy() {
+    static const int per_cu = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, bp_group_kernel<T, METHOD, DR, DC>, 64 * grp_waves<T>(),
+                                                         0) != hipSuccess)
+            v = 1;
+        return std::max(v, 1);
+    }();
+    return per_cu;
+}
+
+// resident slot groups per CU of the instantiation launch_group_shape picks
+static int group_per_cu(const DevGraph& g, int method, size_t tsz) {
+    const bool r8 = g.max_rdeg <= 8, c4 = g.max_cdeg <= 4;
+#define QDEC_GOCC(T, M)                                                          \
+    return r8 ? (c4 ? group_occupancy<T, M, 8, 4>() : group_occupancy<T, M, 8, 8>()) \
+              : (c4 ? group_occupancy<T, M, 16, 4>() : group_occupancy<T, M, 16, 8>())
+    if (tsz == 4) {
+        if (method == 1) QDEC_GOCC(float, 1);
+        QDEC_GOCC(float, 0);
+    }
+    if (method == 1) QDEC_GOCC(double, 1);
+    QDEC_GOCC(double, 0);
+#undef QDEC_GOCC
+}
+
+// Groups in flight: as many as the kernel's occupancy keeps resident, capped by
+// the scratch budget and by the batch (every slot should see >= 2 shots, so the
+// tail of a launch stays short and small test batches stay small).  The
+// scratch is sized from exactly this count (block_scratch_bytes).
+static int64_t group_count(const DevGraph& g, int method, size_t tsz, int num_cus, int64_t B) {
     const size_t per = group_layout(g, tsz).total;
-    const int waves = tsz == 4 ? grp_waves<float>() : grp_waves<double>();
-    int64_t c = std::min<int64_t>((int64_t)num_cus * (32 / waves), (int64_t)(group_scratch_budget() / per));
+    int64_t c = std::min<int64_t>((int64_t)num_cus * group_per_cu(g, method, tsz),
+                                  (int64_t)(group_scratch_budget() / per));
     c = std::min<int64_t>(c, (B + 127) / 128);
     return std::max<int64_t>(c, 1);
 }
@@ -1518,7 +1551,7 @@ static int launch_group_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
     int64_t grid = std::min<int64_t>((int64_t)num_cus * per_cu, max_groups);
-    grid = std::min<int64_t>(grid, group_count(g, sizeof(T), num_cus, a.B));
+    grid = std::min<int64_t>(grid, group_count(g, METHOD, sizeof(T), num_cus, a.B));
     if (grid <= 0) return (int)hipErrorOutOfMemory;
     e = hipMemsetAsync(base, 0, sizeof(unsigned long long), stream);  // shot counter
     if (e != hipSuccess) return (int)e;
@@ -1528,6 +1561,7 @@ static int launch_group_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
         if (e != hipSuccess) return (int)e;
     }
     record_ev(a, 0, stream);
+    QDEC_NOTE_BP("qdec::bp_group_kernel", tname<T>(), METHOD, DR, DC);
     hipLaunchKernelGGL((bp_group_kernel<T, METHOD, DR, DC>), dim3((unsigned)grid), dim3(kGrpThreads), 0, stream, g, a,
                        base, gb, g.row_ptr, g.col_idx, g.col_ptr, g.col_edge, g.edge_csc,
                        reinterpret_cast<const T*>(g.prior[METHOD][sizeof(T) == 4 ? 1 : 0]),
@@ -1560,7 +1594,7 @@ size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num
                                                              getenv("QDEC_GROUP_KERNEL")[0] == '1'))) {
         const size_t fin = (a.ssf && block_placement(g, tsz) == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g)
                                                                   : 0;
-        return kGrpHeader + (size_t)group_count(g, tsz, num_cus, a.B) * group_layout(g, tsz).total + fin;
+        return kGrpHeader + (size_t)group_count(g, method, tsz, num_cus, a.B) * group_layout(g, tsz).total + fin;
     }
     const int placement = block_placement(g, tsz);
     if (placement == 3) return 0;
@@ -1568,6 +1602,21 @@ size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num
     // shot state when it lives in HBM)
     const size_t fin = (a.ssf && placement == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
     return kGrpHeader + (size_t)num_cus * 4 * block_slice_bytes(g, tsz, placement) + fin;
+}
+
+// The smallest scratch a launch can run with (one slot group, or one workgroup
+// slice per CU); block_scratch_bytes' figure may be cut down to it when the
+// allocation fails (fewer groups / slices in flight, same results).
+size_t block_scratch_floor(const DevGraph& g, int method, int precision, int num_cus, const DecodeArgs& a) {
+    const size_t full = block_scratch_bytes(g, method, precision, num_cus, a);
+    if (full == 0) return 0;
+    const size_t tsz = precision == 1 ? 4 : 8;
+    const size_t fin = (a.ssf && block_placement(g, tsz) == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
+    if (group_kernel_applies(g, method, precision, a) && !(lds_kernel_applies(g, method, precision, a) &&
+                                                           !(getenv("QDEC_GROUP_KERNEL") &&
+                                                             getenv("QDEC_GROUP_KERNEL")[0] == '1')))
+        return std::min(full, kGrpHeader + group_layout(g, tsz).total + fin);
+    return full;  // workgroup slices: the launch needs its per-CU slices
 }
 
 int launch_decode_block(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,

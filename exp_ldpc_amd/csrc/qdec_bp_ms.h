@@ -242,6 +242,228 @@ struct ShotSeq {
     }
 };
 
+// The per-wave part shared by the min-sum wave kernels: this lane's slot and
+// state tables, and BP iterations on the wave's LDS rows.  D3R: leading
+// variable rounds whose slots all have degree <= 3.  LEAN: the kernel writes no
+// llr (Q is not kept) and may use the sign-bit check pass.
+template <typename T, int RC, int RV, int DRC, bool LEAN, int D3R>
+struct MsCore {
+    static_assert(DRC <= kDR, "compute width exceeds the LDS row");
+    static_assert(D3R <= RV, "degree rounds");
+    using V2 = __attribute__((ext_vector_type(2))) T;
+    static constexpr int DRS = MsLds<T>::DRS;
+    // the variable pass runs rounds in pairs (2p, 2p+1) on packed fp32 pairs;
+    // an odd last round pairs with itself.  D3P: leading 3-edge rounds, whole pairs.
+    static constexpr int NP = (RV + 1) / 2;
+    static constexpr int D3P = D3R & ~1;
+    static constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
+    static constexpr bool SB = sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT;
+
+    uint32_t etab[RV][kDC];      // v2c element | state index << 16 (edges k < kd(rv))
+    V2 L[NP];                    // priors of rounds (2p, 2p+1)
+    uint32_t vsl[(RV + 1) / 2];  // columns of this lane's slots, u16 pairs
+    int sslot[RC];               // where this lane's checks write their state (host-placed)
+    uint64_t smask[RC][RV];      // slots of this lane's checks' columns, per 64-slot word
+
+    __device__ __forceinline__ void load(const DevGraph& g, int lane) {
+        const T* prior = reinterpret_cast<const T*>(g.ms_prior[PREC]);
+#pragma unroll
+        for (int rv = 0; rv < RV; ++rv) {
+            const int sl = rv * 64 + lane;
+            if (rv % 2 == 0) L[rv / 2].x = L[rv / 2].y = prior[sl];
+            else L[rv / 2].y = prior[sl];
+#pragma unroll
+            for (int k = 0; k < kDC; ++k) etab[rv][k] = (rv < D3P && k == 3) ? 0u : g.ms_etab[PREC][k * g.n_pad + sl];
+            if (rv % 2 == 0) vsl[rv / 2] = g.ms_vslot[sl];
+            else vsl[rv / 2] |= (uint32_t)g.ms_vslot[sl] << 16;
+        }
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) sslot[rc] = g.ms_sslot[PREC][rc * 64 + lane];
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc)
+#pragma unroll
+            for (int w = 0; w < RV; ++w) smask[rc][w] = g.ms_smask[(size_t)w * g.m_pad + rc * 64 + lane];
+    }
+    __device__ __forceinline__ int col_of(int rv) const { return (int)((vsl[rv / 2] >> (16 * (rv % 2))) & 0xffffu); }
+
+    // one-time LDS init: unused row positions hold Big forever (never the
+    // minimum, positive sign), state m_pad is the zero state of pad edges
+    __device__ __forceinline__ static void init_lds(const DevGraph& g, T* v2c, T* st, uint8_t* xh, int lane) {
+        for (int e = lane; e < (int)MsLds<T>::v2c_elems(MsLds<T>::rows(g)); e += 64) v2c[e] = Big<T>::v;
+        for (int e = lane; e < (int)MsLds<T>::state_elems(g.m_pad); e += 64) st[e] = (T)0;
+        for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
+    }
+
+    // initial messages: v2c = prior
+    __device__ __forceinline__ void write_priors(T* v2c) const {
+#pragma unroll
+        for (int rv = 0; rv < RV; ++rv)
+#pragma unroll
+            for (int k = 0; k < kDC; ++k)
+                if (!(rv < D3P && k == 3)) v2c[etab[rv][k] & 0xffff] = (rv % 2 == 0) ? L[rv / 2].x : L[rv / 2].y;
+    }
+
+    // BP iterations it, it + 1, .. max_iter on rows holding the priors
+    // (write_priors, then a wave_lds_sync).  Returns true when the syndrome is
+    // met (`it` = that iteration); X: hard decisions by slot (ballot words),
+    // pres: the residual syndrome bit of this lane's checks, Q: posteriors (!LEAN).
+    __device__ __forceinline__ bool iterate(const DecodeArgs& a, T* v2c, T* st, int m, int lane, const bool (&sbit)[RC],
+                                            T (&Q)[RV], uint64_t (&X)[RV], bool (&pres)[RC], int& it) const {
+        V2 vp[NP][kDC];  // v2c messages this lane sent last iteration, round pairs
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int k = 0; k < kDC; ++k) vp[p][k] = L[p];
+        for (; it <= a.max_iter; ++it) {
+            const T alpha = alpha_bits<T>(it, a.ms_scaling);
+            // ---- check pass: state (m1, m2) with the parity in both signs ----
+            uint32_t zrows = 0;  // rows holding a zero entry (sign-bit parity inexact)
+#pragma unroll
+            for (int rc = 0; rc < RC; ++rc) {
+                const int i = min(rc * 64 + lane, m);  // pad check lanes share the Big row m
+                T v[kDR];
+                // odd f64 rows load only their DRC slots (r03i A/B: -0.5% BP kernel time)
+                if constexpr (sizeof(T) == 8 && DRC % 2 == 1) lds_load_first<T, DRC>(v2c + i * DRS, v);
+                else lds_load<T, kDR>(v2c + i * DRS, v);
+                T m1 = Big<T>::v, m2 = Big<T>::v;
+                bool par = sbit[rc];
+                if constexpr (sizeof(T) == 4) {
+#pragma unroll
+                    for (int k = 0; k < DRC; ++k) {
+                        const T av = fabs(v[k]);
+                        m2 = med3(av, m1, m2);
+                        m1 = med3(av, m1, -Big<T>::v);  // true median = min(|v|, m1): one VALU, abs modifier
+                    }
+                } else {
+                    // f64: (minimum, second minimum) of |v| by a merge tree instead of a
+                    // sequential chain (17 instead of 21 f64 ops for 7 values, depth 5
+                    // instead of 14); the same two values, so bit-identical
+                    const Top2 t = top2_tree<0, DRC>(v);
+                    m1 = t.lo;
+                    m2 = t.hi;
+                }
+                V2 s2;
+                if constexpr (SB) {
+                    // sign-canonical row: the parity is the XOR of the sign bits
+                    uint32_t hx = par ? 0x80000000u : 0u;
+                    int k = 0;
+#pragma unroll
+                    for (; k + 1 < DRC; k += 2) hx = __builtin_amdgcn_bitop3_b32(hx, f64_hi(v[k]), f64_hi(v[k + 1]), 0x96);
+                    if (k < DRC) hx ^= f64_hi(v[k]);
+                    // m1, m2 >= +0: the XOR of the parity bit sets their sign bit
+                    s2.x = f64_xor_sign(m1, hx);
+                    s2.y = f64_xor_sign(m2, hx);
+                    if (m1 == (T)0) zrows |= 1u << rc;  // a zero entry: fixed below
+                } else {
+#pragma unroll
+                    for (int k = 0; k < DRC; ++k)
+                        par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign (s_xor of compare masks)
+                    // both minima carry the parity in their sign bit (they are >= +0)
+                    s2.x = par ? -m1 : m1;
+                    s2.y = par ? -m2 : m2;
+                }
+                *reinterpret_cast<V2*>(st + 2 * sslot[rc]) = s2;
+            }
+            if constexpr (SB) {
+                if (__ballot(zrows != 0u)) {  // rare (wave-uniform): rows with a zero entry, parity by the compares
+                    asm volatile("" ::: "memory");  // re-read the row and the state just written
+#pragma unroll
+                    for (int rc = 0; rc < RC; ++rc)
+                        if ((zrows >> rc) & 1u)
+                            ms_zero_row_fix<DRC>((lds_f64*)(v2c + min(rc * 64 + lane, m) * DRS), sbit[rc],
+                                                 (lds_f64*)(st + 2 * sslot[rc]));
+                }
+            }
+            wave_lds_sync();
+
+            // ---- variable pass, rounds in pairs (the next pair's states are
+            // gathered while this pair sums) ----
+            auto gather = [&](int p, V2 (&sa)[kDC], V2 (&sb)[kDC]) {
+                const int r0 = 2 * p, r1 = 2 * p + 1 < RV ? 2 * p + 1 : 2 * p;
+#pragma unroll
+                for (int k = 0; k < kDC; ++k)
+                    if (!(r1 < D3P && k == 3)) {
+                        sa[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[r0][k] >> 16));
+                        if (r1 != r0) sb[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[r1][k] >> 16));
+                    }
+            };
+            V2 sa[kDC], sb[kDC];
+            gather(0, sa, sb);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const int r0 = 2 * p, r1 = 2 * p + 1 < RV ? 2 * p + 1 : 2 * p;
+                const int KD = r1 < D3P ? 3 : kDC;
+                // |c| = alpha * ((|v| == m1) ? m2 : m1), sign = parity ^ (v <= 0);
+                // the state's signs carry the parity, so one select picks both
+                V2 y[kDC];
+#pragma unroll
+                for (int k = 0; k < kDC; ++k) {
+                    if (k < KD) {
+                        y[k].x = (fabs(vp[p][k].x) == fabs(sa[k].x)) ? sa[k].y : sa[k].x;
+                        const V2 sbk = r1 != r0 ? sb[k] : sa[k];
+                        y[k].y = (fabs(vp[p][k].y) == fabs(sbk.x)) ? sbk.y : sbk.x;
+                    }
+                }
+                if (p + 1 < NP) gather(p + 1 < NP ? p + 1 : p, sa, sb);
+                V2 c[kDC];
+#pragma unroll
+                for (int k = 0; k < kDC; ++k) {
+                    if (k < KD) {
+                        const V2 yk = y[k] * alpha;
+                        if constexpr (SB) {
+                            c[k].x = f64_xor_sign(yk.x, f64_hi(vp[p][k].x));
+                            c[k].y = f64_xor_sign(yk.y, f64_hi(vp[p][k].y));
+                        } else {
+                            c[k].x = (vp[p][k].x <= (T)0) ? -yk.x : yk.x;
+                            c[k].y = (vp[p][k].y <= (T)0) ? -yk.y : yk.y;
+                        }
+                    }
+                }
+                V2 pre[kDC];
+                V2 acc = L[p];
+#pragma unroll
+                for (int k = 0; k < kDC; ++k) {
+                    if (k < KD) {
+                        pre[k] = acc;
+                        acc += c[k];
+                    }
+                }
+                if constexpr (!LEAN) {
+                    Q[r0] = acc.x;
+                    Q[r1] = acc.y;
+                }
+                X[r0] = __ballot(acc.x <= (T)0);
+                if (r1 != r0) X[r1] = __ballot(acc.y <= (T)0);
+                // ldpc: out_k = pre_k + (sum of the later c); the last one adds an
+                // empty sum (+0), which can only turn -0 into +0: both are <= 0 and
+                // have |v| = 0, so the message is used identically either way
+                V2 suf;
+#pragma unroll
+                for (int k = kDC - 1; k >= 0; --k) {
+                    if (k < KD) {
+                        const V2 out = (k == KD - 1) ? pre[k] : pre[k] + suf;
+                        suf = (k == KD - 1) ? c[k] : suf + c[k];
+                        vp[p][k] = out;
+                        v2c[etab[r0][k] & 0xffff] = out.x;  // pads -> dummy element
+                        if (r1 != r0) v2c[etab[r1][k] & 0xffff] = out.y;
+                    }
+                }
+            }
+
+            // ---- syndrome test (registers only) ----
+            int bad = 0;
+#pragma unroll
+            for (int rc = 0; rc < RC; ++rc) {
+                pres[rc] = sbit[rc] != (masked_parity<RV>(smask[rc], X) != 0);
+                bad |= pres[rc];
+            }
+            wave_lds_sync();  // v2c scatter complete before the next check pass
+            if (__ballot(bad) == 0ull) return true;
+        }
+        return false;
+    }
+};
+
 // LEAN: the throughput configuration (no x / corr / llr outputs, no base, no
 // syndrome flags, no spacetime fold): the per-shot epilogue is the ballot-word
 // failure check only, which keeps the kernel's scalar state small.
@@ -254,16 +476,9 @@ struct ShotSeq {
 // waves per CU (qd_graph_set_wave_occupancy: the bench's concurrent points).
 template <typename T, int RC, int RV, int DRC, bool DEFER, bool LEAN, int D3R, int OCC = 0>
 __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void bp_ms_wave_kernel(DevGraph g, DecodeArgs a) {
-    static_assert(DRC <= kDR, "compute width exceeds the LDS row");
-    static_assert(D3R <= RV, "degree rounds");
-    using V2 = __attribute__((ext_vector_type(2))) T;
     using Io = ShotIo<RC, RV>;
-    constexpr int DRS = MsLds<T>::DRS;
-    // the variable pass runs rounds in pairs (2p, 2p+1) on packed fp32 pairs;
-    // an odd last round pairs with itself.  D3P: leading 3-edge rounds, whole pairs.
-    constexpr int NP = (RV + 1) / 2;
-    constexpr int D3P = D3R & ~1;
-    constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
+    using Core = MsCore<T, RC, RV, DRC, LEAN, D3R>;
+    constexpr int PREC = Core::PREC;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* v2c = reinterpret_cast<T*>(smem);
     T* st = v2c + MsLds<T>::v2c_elems(MsLds<T>::rows(g));
@@ -272,41 +487,15 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
 
     const int lane = threadIdx.x;
     const int m = g.m, n = g.n;
-    const T* prior = reinterpret_cast<const T*>(g.ms_prior[PREC]);
-
-    uint32_t etab[RV][kDC];  // v2c element | state index << 16 (edges k < kd(rv))
-    V2 L[NP];                // priors of rounds (2p, 2p+1)
-    uint32_t vsl[(RV + 1) / 2];  // columns of this lane's slots, u16 pairs
-#pragma unroll
-    for (int rv = 0; rv < RV; ++rv) {
-        const int sl = rv * 64 + lane;
-        if (rv % 2 == 0) L[rv / 2].x = L[rv / 2].y = prior[sl];
-        else L[rv / 2].y = prior[sl];
-#pragma unroll
-        for (int k = 0; k < kDC; ++k) etab[rv][k] = (rv < D3P && k == 3) ? 0u : g.ms_etab[PREC][k * g.n_pad + sl];
-        if (rv % 2 == 0) vsl[rv / 2] = g.ms_vslot[sl];
-        else vsl[rv / 2] |= (uint32_t)g.ms_vslot[sl] << 16;
-    }
-    auto col_of = [&](int rv) -> int { return (int)((vsl[rv / 2] >> (16 * (rv % 2))) & 0xffffu); };
-    int sslot[RC];  // where this lane's checks write their state (host-placed)
-#pragma unroll
-    for (int rc = 0; rc < RC; ++rc) sslot[rc] = g.ms_sslot[PREC][rc * 64 + lane];
+    Core core;
+    core.load(g, lane);
     // zero syndrome + every prior > 0: iteration 1 converges with x = 0 (all
     // messages are >= 0, so every posterior is >= its prior > 0), and the LEAN
     // outputs (iterations 1, converged, failure from the readout alone) need
     // nothing else
     const bool zero_ok = LEAN && ((g.ms_allpos >> PREC) & 1);
-    uint64_t smask[RC][RV];
-#pragma unroll
-    for (int rc = 0; rc < RC; ++rc)
-#pragma unroll
-        for (int w = 0; w < RV; ++w) smask[rc][w] = g.ms_smask[(size_t)w * g.m_pad + rc * 64 + lane];
 
-    // one-time LDS init: unused row positions hold Big forever (never the
-    // minimum, positive sign), state m_pad is the zero state of pad edges
-    for (int e = lane; e < (int)MsLds<T>::v2c_elems(MsLds<T>::rows(g)); e += 64) v2c[e] = Big<T>::v;
-    for (int e = lane; e < (int)MsLds<T>::state_elems(g.m_pad); e += 64) st[e] = (T)0;
-    for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
+    Core::init_lds(g, v2c, st, xh, lane);
     io.init(g, lane);
     ShotSeq seq(a, lane);
     int64_t shot = seq.next(lane);
@@ -378,7 +567,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
             uint64_t Xf[RV];
 #pragma unroll
             for (int w = 0; w < RV; ++w) {
-                const int q = col_of(w);
+                const int q = core.col_of(w);
                 int v = 0;
                 if (q < g.n_data) {
                     if (use_b) v ^= a.base[shot * g.n_data + q];
@@ -390,18 +579,12 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
             for (int rc = 0; rc < RC; ++rc) {
                 uint64_t acc = 0;
 #pragma unroll
-                for (int w = 0; w < RV; ++w) acc ^= smask[rc][w] & Xf[w];
+                for (int w = 0; w < RV; ++w) acc ^= core.smask[rc][w] & Xf[w];
                 sbit[rc] ^= (__popcll(acc) & 1) != 0;
             }
         }
 
-        // ---- initial messages: v2c = prior (held in registers as vp and
-        // written to the rows unless the shot is skipped) ----
-        V2 vp[NP][kDC];  // v2c messages this lane sent last iteration, round pairs
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-#pragma unroll
-            for (int k = 0; k < kDC; ++k) vp[p][k] = L[p];
+        // ---- initial messages: v2c = prior, unless the shot is skipped ----
         bool skip = false;
         if (zero_ok) {
             bool any = false;
@@ -409,13 +592,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
             for (int rc = 0; rc < RC; ++rc) any |= sbit[rc];
             skip = __ballot(any) == 0ull;
         }
-        if (!skip) {
-#pragma unroll
-            for (int rv = 0; rv < RV; ++rv)
-#pragma unroll
-                for (int k = 0; k < kDC; ++k)
-                    if (!(rv < D3P && k == 3)) v2c[etab[rv][k] & 0xffff] = (rv % 2 == 0) ? L[rv / 2].x : L[rv / 2].y;
-        }
+        if (!skip) core.write_priors(v2c);
         wave_lds_sync();
 
         QDEC_STAMP(1);
@@ -443,163 +620,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) pres[rc] = false;
         }
-        for (; !kSkipBp && !skip && it <= a.max_iter; ++it) {
-            const T alpha = alpha_bits<T>(it, a.ms_scaling);
-            // ---- check pass: state (m1, m2) with the parity in both signs ----
-            uint32_t zrows = 0;  // rows holding a zero entry (sign-bit parity inexact)
-#pragma unroll
-            for (int rc = 0; rc < RC; ++rc) {
-                const int i = min(rc * 64 + lane, m);  // pad check lanes share the Big row m
-                T v[kDR];
-                // odd f64 rows load only their DRC slots (r03i A/B: -0.5% BP kernel time)
-                if constexpr (sizeof(T) == 8 && DRC % 2 == 1) lds_load_first<T, DRC>(v2c + i * DRS, v);
-                else lds_load<T, kDR>(v2c + i * DRS, v);
-                T m1 = Big<T>::v, m2 = Big<T>::v;
-                bool par = sbit[rc];
-                if constexpr (sizeof(T) == 4) {
-#pragma unroll
-                    for (int k = 0; k < DRC; ++k) {
-                        const T av = fabs(v[k]);
-                        m2 = med3(av, m1, m2);
-                        m1 = med3(av, m1, -Big<T>::v);  // true median = min(|v|, m1): one VALU, abs modifier
-                    }
-                } else {
-                    // f64: (minimum, second minimum) of |v| by a merge tree instead of a
-                    // sequential chain (17 instead of 21 f64 ops for 7 values, depth 5
-                    // instead of 14); the same two values, so bit-identical
-                    const Top2 t = top2_tree<0, DRC>(v);
-                    m1 = t.lo;
-                    m2 = t.hi;
-                }
-                V2 s2;
-                constexpr bool SB = sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT;
-                if constexpr (SB) {
-                    // sign-canonical row: the parity is the XOR of the sign bits
-                    uint32_t hx = par ? 0x80000000u : 0u;
-                    int k = 0;
-#pragma unroll
-                    for (; k + 1 < DRC; k += 2) hx = __builtin_amdgcn_bitop3_b32(hx, f64_hi(v[k]), f64_hi(v[k + 1]), 0x96);
-                    if (k < DRC) hx ^= f64_hi(v[k]);
-                    // m1, m2 >= +0: the XOR of the parity bit sets their sign bit
-                    s2.x = f64_xor_sign(m1, hx);
-                    s2.y = f64_xor_sign(m2, hx);
-                    if (m1 == (T)0) zrows |= 1u << rc;  // a zero entry: fixed below
-                } else {
-#pragma unroll
-                    for (int k = 0; k < DRC; ++k)
-                        par ^= v[k] <= (T)0;  // ldpc: bit_to_check <= 0 flips the sign (s_xor of compare masks)
-                    // both minima carry the parity in their sign bit (they are >= +0)
-                    s2.x = par ? -m1 : m1;
-                    s2.y = par ? -m2 : m2;
-                }
-                *reinterpret_cast<V2*>(st + 2 * sslot[rc]) = s2;
-            }
-            if constexpr (sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT) {
-#ifdef QDEC_STAMPS
-                {  // dev counters: wave-iterations with a zero row, zero-row lanes
-                    const unsigned long long zb = __ballot(zrows != 0u);
-                    QDEC_COUNT(13, zb != 0ull);
-                    QDEC_COUNT(14, __popcll(zb));
-                }
-#endif
-                if (__ballot(zrows != 0u)) {  // rare (wave-uniform): rows with a zero entry, parity by the compares
-                    asm volatile("" ::: "memory");  // re-read the row and the state just written
-#pragma unroll
-                    for (int rc = 0; rc < RC; ++rc)
-                        if ((zrows >> rc) & 1u)
-                            ms_zero_row_fix<DRC>((lds_f64*)(v2c + min(rc * 64 + lane, m) * DRS), sbit[rc],
-                                                 (lds_f64*)(st + 2 * sslot[rc]));
-                }
-            }
-            wave_lds_sync();
-
-            // ---- variable pass, rounds in pairs (the next pair's states are
-            // gathered while this pair sums) ----
-            auto gather = [&](int p, V2 (&sa)[kDC], V2 (&sb)[kDC]) {
-                const int r0 = 2 * p, r1 = 2 * p + 1 < RV ? 2 * p + 1 : 2 * p;
-#pragma unroll
-                for (int k = 0; k < kDC; ++k)
-                    if (!(r1 < D3P && k == 3)) {
-                        sa[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[r0][k] >> 16));
-                        if (r1 != r0) sb[k] = *reinterpret_cast<const V2*>(st + 2 * (etab[r1][k] >> 16));
-                    }
-            };
-            V2 sa[kDC], sb[kDC];
-            gather(0, sa, sb);
-#pragma unroll
-            for (int p = 0; p < NP; ++p) {
-                const int r0 = 2 * p, r1 = 2 * p + 1 < RV ? 2 * p + 1 : 2 * p;
-                const int KD = r1 < D3P ? 3 : kDC;
-                // |c| = alpha * ((|v| == m1) ? m2 : m1), sign = parity ^ (v <= 0);
-                // the state's signs carry the parity, so one select picks both
-                V2 y[kDC];
-#pragma unroll
-                for (int k = 0; k < kDC; ++k) {
-                    if (k < KD) {
-                        y[k].x = (fabs(vp[p][k].x) == fabs(sa[k].x)) ? sa[k].y : sa[k].x;
-                        const V2 sbk = r1 != r0 ? sb[k] : sa[k];
-                        y[k].y = (fabs(vp[p][k].y) == fabs(sbk.x)) ? sbk.y : sbk.x;
-                    }
-                }
-                if (p + 1 < NP) gather(p + 1 < NP ? p + 1 : p, sa, sb);
-                V2 c[kDC];
-#pragma unroll
-                for (int k = 0; k < kDC; ++k) {
-                    if (k < KD) {
-                        const V2 yk = y[k] * alpha;
-                        if constexpr (sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT) {
-                            c[k].x = f64_xor_sign(yk.x, f64_hi(vp[p][k].x));
-                            c[k].y = f64_xor_sign(yk.y, f64_hi(vp[p][k].y));
-                        } else {
-                            c[k].x = (vp[p][k].x <= (T)0) ? -yk.x : yk.x;
-                            c[k].y = (vp[p][k].y <= (T)0) ? -yk.y : yk.y;
-                        }
-                    }
-                }
-                V2 pre[kDC];
-                V2 acc = L[p];
-#pragma unroll
-                for (int k = 0; k < kDC; ++k) {
-                    if (k < KD) {
-                        pre[k] = acc;
-                        acc += c[k];
-                    }
-                }
-                if constexpr (!LEAN) {
-                    Q[r0] = acc.x;
-                    Q[r1] = acc.y;
-                }
-                X[r0] = __ballot(acc.x <= (T)0);
-                if (r1 != r0) X[r1] = __ballot(acc.y <= (T)0);
-                // ldpc: out_k = pre_k + (sum of the later c); the last one adds an
-                // empty sum (+0), which can only turn -0 into +0: both are <= 0 and
-                // have |v| = 0, so the message is used identically either way
-                V2 suf;
-#pragma unroll
-                for (int k = kDC - 1; k >= 0; --k) {
-                    if (k < KD) {
-                        const V2 out = (k == KD - 1) ? pre[k] : pre[k] + suf;
-                        suf = (k == KD - 1) ? c[k] : suf + c[k];
-                        vp[p][k] = out;
-                        v2c[etab[r0][k] & 0xffff] = out.x;  // pads -> dummy element
-                        if (r1 != r0) v2c[etab[r1][k] & 0xffff] = out.y;
-                    }
-                }
-            }
-
-            // ---- syndrome test (registers only) ----
-            int bad = 0;
-#pragma unroll
-            for (int rc = 0; rc < RC; ++rc) {
-                pres[rc] = sbit[rc] != (masked_parity<RV>(smask[rc], X) != 0);
-                bad |= pres[rc];
-            }
-            wave_lds_sync();  // v2c scatter complete before the next check pass
-            if (__ballot(bad) == 0ull) {
-                conv = true;
-                break;
-            }
-        }
+        if (!kSkipBp && !skip) conv = core.iterate(a, v2c, st, m, lane, sbit, Q, X, pres, it);
         const int iters = conv ? it : a.max_iter;
         QDEC_STAMP(2);
         QDEC_COUNT(8, iters);
@@ -620,12 +641,12 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         }
         // hard decision by column (slot order -> xh[column])
 #pragma unroll
-        for (int rv = 0; rv < RV; ++rv) xh[col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
+        for (int rv = 0; rv < RV; ++rv) xh[core.col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
         if (!LEAN && a.llr_out) {
             T* lo = reinterpret_cast<T*>(a.llr_out);
 #pragma unroll
             for (int rv = 0; rv < RV; ++rv) {
-                const int j = col_of(rv);
+                const int j = core.col_of(rv);
                 if (j < n) lo[shot * n + j] = Q[rv];
             }
         }

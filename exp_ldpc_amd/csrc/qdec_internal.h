@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace qdec {
 
 constexpr int kWave = 64;        // CDNA wavefront
@@ -186,6 +188,41 @@ inline void record_ev(const DecodeArgs& a, int i, hipStream_t s) {
     if (a.ev) (void)hipEventRecord(a.ev[i], s);
 }
 
+// Names of the BP and SSF kernels the calling host thread's last launch_decode
+// enqueued, spelled as rocprofv3 prints them (template arguments included; ""
+// when none / not recorded).  Host only; read by qd_graph_last_kernels.
+struct LaunchNames {
+    const char* bp = "";
+    const char* ssf = "";
+};
+LaunchNames& last_launch_names();
+
+// rocprofv3's spelling of a kernel instantiation: base<arg, arg, ...>
+inline std::string targ(bool b) { return b ? "true" : "false"; }
+inline std::string targ(int v) { return std::to_string(v); }
+inline std::string targ(const char* s) { return s; }
+template <typename T>
+inline const char* tname() { return sizeof(T) == 8 ? "double" : "float"; }
+template <typename... A>
+inline std::string kernel_name(const char* base, A... args) {
+    std::string s = std::string(base) + "<";
+    bool first = true;
+    ((s += (first ? std::string() : std::string(", ")) + targ(args), first = false), ...);
+    return s + ">";
+}
+// record the instantiation (one string per call site and instantiation)
+#define QDEC_NOTE_BP(...)                                           \
+    do {                                                            \
+        static const std::string qdec_kn_ = kernel_name(__VA_ARGS__); \
+        last_launch_names().bp = qdec_kn_.c_str();                  \
+    } while (0)
+#define QDEC_NOTE_SSF(...)                                          \
+    do {                                                            \
+        static const std::string qdec_kn_ = kernel_name(__VA_ARGS__); \
+        last_launch_names().ssf = qdec_kn_.c_str();                 \
+    } while (0)
+
+
 // Launchers (qdec_bp.hip / qdec_sample.hip).  Return hipError_t as int.
 int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a,
                   int num_cus, hipStream_t stream, void* scratch, size_t scratch_bytes);
@@ -193,6 +230,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
                         hipStream_t stream, void* scratch, size_t scratch_bytes);
 int launch_ssf_block(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream);
 size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, const DecodeArgs& a);
+size_t block_scratch_floor(const DevGraph& g, int method, int precision, int num_cus, const DecodeArgs& a);
 bool group_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a);
 bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a);
 int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,

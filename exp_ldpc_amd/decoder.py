@@ -119,6 +119,8 @@ class Decoder:
         failure check; handed over as CSR supports (qd_graph_set_logicals_csr),
         so codes with thousands of sparse logicals never build a dense k x n
         array."""
+        if not sp.issparse(lz) and np.ndim(lz) != 2:  # csr_matrix would read a 1-D array as one row
+            raise ValueError("logicals must be k x n_data")
         L = sp.csr_matrix(lz, copy=True) if sp.issparse(lz) else sp.csr_matrix(np.asarray(lz) % 2)
         if L.ndim != 2 or L.shape[1] != self.n_data:
             raise ValueError("logicals must be k x n_data")
@@ -282,6 +284,14 @@ class Decoder:
         _abi.check(self._lib.qd_graph_read_timing(self._handle, _abi.ptr(bp), _abi.ptr(ssf), cap, C.byref(cnt)),
                    "qd_graph_read_timing")
         return bp[:cnt.value].astype(np.float64), ssf[:cnt.value].astype(np.float64)
+
+    def last_kernels(self) -> tuple[str, str]:
+        """(BP kernel, SSF kernel) the last decode call launched, in rocprofv3's
+        spelling with template arguments ("" for a stage that did not run)."""
+        bp = C.create_string_buffer(512)
+        ssf = C.create_string_buffer(512)
+        _abi.check(self._lib.qd_graph_last_kernels(self._handle, bp, 512, ssf, 512), "qd_graph_last_kernels")
+        return bp.value.decode(), ssf.value.decode()
 
     def close(self) -> None:
         if getattr(self, "_handle", None) and self._handle.value:

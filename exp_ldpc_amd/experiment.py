@@ -44,7 +44,7 @@ from .osd import OsdSolver
 from .spacetime import SpacetimeCode, SpacetimeCodeSingleShot
 from .storage_sim import build_storage_simulation
 
-__all__ = ["DECODER_MODES", "BatchPipeline", "BPOSDCorrect", "BPOSDHybridCorrect", "BPOSDCorrectSingleShot",
+__all__ = ["DECODER_MODES", "BatchPipeline", "ShardError", "run_shards", "BPOSDCorrect", "BPOSDHybridCorrect", "BPOSDCorrectSingleShot",
            "BPSSFCorrect", "BPDetectorCorrect", "run_simulation", "add_bposd_args", "unpack_bposd_args", "load_code", "p_sweep",
            "p_sweep_main", "parse_sweep_spec"]
 
@@ -129,6 +129,12 @@ class BatchPipeline:
             if noise is None or getattr(noise, "kind", "") != "depolarizing":
                 raise NotImplementedError("bpd_detector builds its DEM for depolarizing_noise(p, pm) only")
             from .dem import DetectorSpacetimeCode, storage_experiment_dem
+            if R >= 2:
+                import warnings
+                warnings.warn("bpd_detector at rounds >= 2 decodes the storage experiment's Z-sector DEM, not Stim's "
+                              "two-sector circuit DEM the reference uses (_experiment.py:174,186): its LER is not "
+                              "reference-equivalent (unpinned without Stim; dem.storage_experiment_dem)",
+                              RuntimeWarning, stacklevel=2)
             self.dem = DetectorSpacetimeCode(storage_experiment_dem(self.H, self.L, R, noise.p, noise.pm))
             fmap = self.dem.fault_map.toarray() % 2
             self.n_faults = self.dem.fault_priors.size
@@ -138,6 +144,10 @@ class BatchPipeline:
         self.sampler_graph = Decoder(self.H, 0.01, device=self.device)
 
     # ----------------------------------------------------------- helpers
+    def decoders(self):
+        """The BP decoders this pipeline launches (for the timing ring)."""
+        return [d for d in (getattr(self, k, None) for k in ("st", "fin", "ss", "det")) if d is not None]
+
     def _fail_host(self, readout, corr):
         if self.L.shape[0] == 0:
             return np.zeros(readout.shape[0], bool)
@@ -479,13 +489,77 @@ def _append_checkpoint_row(path, point) -> None:
     os.replace(tmp, path)
 
 
+class ShardError(RuntimeError):
+    """A shot range that failed twice (once, then once more in a fresh worker)."""
+
+    def __init__(self, p_ph, device, lo, hi, cause):
+        super().__init__(f"p_sweep shard failed twice: p={p_ph!r}, device {device}, shots [{lo}, {hi}): {cause!r}")
+        self.p_ph, self.device, self.lo, self.hi, self.cause = p_ph, device, lo, hi, cause
+
+
+def run_shards(shards, work, p_ph=None, retries: int = 1):
+    """Run work(device, lo, hi, attempt) -> counters for every (device, lo, hi)
+    shard, one host thread per shard (each blocks on its own device's copies),
+    and sum the counters.  A shard that raises is run again in a fresh worker
+    thread on the same device (its handles rebuilt by `work` when attempt > 0;
+    never a re-exec of a process that touched the GPU), up to `retries` times;
+    then ShardError names the point and the failed shot range.  The reference
+    fan-out (misc/p_sweep.py:24-40, Pool.starmap) aborts the sweep on any
+    worker exception."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def attempt(i, k):
+        d, lo, hi = shards[i]
+        return work(d, lo, hi, k)
+
+    results = [None] * len(shards)
+    pending = list(range(len(shards)))
+    for k in range(retries + 1):
+        errors = {}
+        if len(pending) == 1 and k == 0:  # the common 1-device case: no thread
+            try:
+                results[pending[0]] = attempt(pending[0], 0)
+            except Exception as e:  # noqa: BLE001 - retried below, then reported with its range
+                errors[pending[0]] = e
+        else:
+            with ThreadPoolExecutor(max_workers=len(pending)) as ex:  # fresh threads every attempt
+                futs = {i: ex.submit(attempt, i, k) for i in pending}
+                for i, f in futs.items():
+                    try:
+                        results[i] = f.result()
+                    except Exception as e:  # noqa: BLE001
+                        errors[i] = e
+        if not errors:
+            break
+        pending = sorted(errors)
+        if k == retries:
+            i = pending[0]
+            d, lo, hi = shards[i]
+            raise ShardError(p_ph, d, lo, hi, errors[i]) from errors[i]
+    n = max(len(r) for r in results)
+    return [sum(r[j] for r in results) for j in range(n)]
+
+
+HBM_PEAK_BYTES_S = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
 def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_prior, *, gpus: int | None = None,
-            seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f64", checkpoint: str | None = None,
-            **kwargs):
+            devices=None, seed: int = DEFAULT_SEED, batch: int = 1 << 18, precision: str = "f64",
+            checkpoint: str | None = None, **kwargs):
     """Sweep the physical error rate (reference p_sweep, misc/p_sweep.py:17-40).
-    Shots are sharded over `gpus` devices by index (device d decodes a
-    contiguous shot range); exactly `samples` shots per point.  BP runs in
-    `precision` (default f64, ldpc v1's message precision); every row records it.
+    Shots are sharded over `gpus` devices by index (shard d decodes a
+    contiguous shot range); exactly `samples` shots per point.  `devices`
+    (a list of device ordinals, repeats allowed) overrides `gpus`: one shard per
+    entry.  BP runs in `precision` (default f64, ldpc v1's message precision);
+    every row records it.  A failed shard is retried once in a fresh worker
+    thread (run_shards); a second failure raises ShardError with its range.
+
+    Per point, besides the reference's columns: shots_per_s, bp_converged_frac,
+    iters_mean, ssf_steps_mean, and from the library's HIP-event timing ring
+    kernel_ms (summed over shards and decode stages), hbm_bytes (the compulsory
+    per-shot I/O: syndrome + readout in, failure flag out) and
+    hbm_roofline_frac = hbm_bytes / kernel time / HBM peak (summed kernel time:
+    shards on distinct devices overlap, so this is per device-second).
 
     checkpoint: CSV path; each finished point is appended to it at once, and a
     restarted sweep reuses a row only when its p and its configuration
@@ -496,7 +570,8 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
     import pandas as pd
     torch = _torch()
     done = _load_checkpoint(checkpoint)
-    ndev = gpus or _device_count()
+    devs = [int(d) for d in devices] if devices else list(range(gpus or _device_count()))
+    ndev = len(devs)
     code = kwargs["code"]
     rounds = kwargs["rounds"]
     mode = kwargs["decoder_mode"]
@@ -516,15 +591,24 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
         t0 = time.perf_counter()
         nm = noise_model(**nm_args)
         sim = build_storage_simulation(rounds, nm, code, use_x_logicals=False)
-        pipes = [BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision, noise=nm)
-                 for d in range(ndev)]
-        per = math.ceil(samples / ndev)
 
-        def shard(d):
-            """Device d's contiguous shot range; returns its counters."""
-            pipe = pipes[d]
-            lo, hi = d * per, min(samples, (d + 1) * per)
-            acc = [0, 0, 0, 0]
+        def pipeline(d):
+            return BatchPipeline(code, rounds, mode, bp_osd_options, (dp, mp), device=d, precision=precision,
+                                 noise=nm)
+        pipes = [pipeline(d) for d in devs]
+        per = math.ceil(samples / ndev)
+        shards = [(i, i * per, min(samples, (i + 1) * per)) for i in range(ndev)]
+
+        def shard(i, lo, hi, attempt):
+            """Shard i's contiguous shot range on device devs[i]; returns its
+            counters (failures, converged, iterations, SSF steps, kernel ms)."""
+            d = devs[i]
+            pipe = pipes[i] if attempt == 0 else pipeline(d)  # a retry rebuilds its handles
+            nb = max(1, -(-(hi - lo) // batch))
+            decs = pipe.decoders()
+            for dec in decs:
+                dec.set_timing(nb)
+            acc = [0, 0, 0, 0, 0.0]
             with torch.cuda.device(d):
                 for start in range(lo, hi, batch):
                     b = min(batch, hi - start)
@@ -535,27 +619,29 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
                     acc[2] += res.iters_sum
                     acc[3] += res.ssf_steps_sum
                 torch.cuda.synchronize(d)
+            for dec in decs:
+                bp, ssf = dec.read_timing()
+                acc[4] += float(bp.sum() + ssf.sum())
             return acc
 
-        if ndev == 1:
-            parts = [shard(0)]
-        else:  # one host thread per device: each pipeline blocks on its own D2H copies
-            from concurrent.futures import ThreadPoolExecutor
-            with ThreadPoolExecutor(max_workers=ndev) as ex:
-                parts = list(ex.map(shard, range(ndev)))
-        failures, conv, iters, ssf = (sum(p[i] for p in parts) for i in range(4))
+        failures, conv, iters, ssf, kernel_ms = run_shards(shards, shard, p_ph=p_ph)
         runtime = time.perf_counter() - t0
+        hbm = samples * ((rounds + 1) * pipes[0].m + pipes[0].n + 1)
         point = {"p_ph": p_ph, "failures": failures, "samples": samples, "walltime": runtime, **kwargs,
                  **bp_osd_options, "gpus": ndev, "shots_per_s": samples / runtime if runtime > 0 else float("nan"),
                  "bp_converged_frac": conv / samples if samples else 0.0,
                  "iters_mean": iters / samples if samples else 0.0,
-                 "ssf_steps_mean": ssf / samples if samples else 0.0}
+                 "ssf_steps_mean": ssf / samples if samples else 0.0,
+                 "kernel_ms": kernel_ms, "hbm_bytes": hbm,
+                 "hbm_roofline_frac": hbm / (kernel_ms * 1e-3) / HBM_PEAK_BYTES_S if kernel_ms > 0 else float("nan")}
         del point["code"]
         del point["bp_osd_options"]
         point["seed"] = seed
         point["precision"] = precision
         point["point_index"] = pi
         point["config_fp"] = fp
+        if mode == "bpd_detector" and rounds >= 2:
+            point["dem_sector"] = "z_only_unpinned"  # see BatchPipeline's warning / dem.storage_experiment_dem
         data.append(point)
         if checkpoint:
             _append_checkpoint_row(checkpoint, point)
@@ -596,6 +682,8 @@ def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
                              "space")
     add_bposd_args(parser)
     parser.add_argument("--gpus", type=int, default=None, help="GPUs to shard shots over (default: all visible)")
+    parser.add_argument("--devices", type=lambda v: [int(x) for x in v.split(",") if x.strip()], default=None,
+                        help="comma-separated device ordinals, one shot shard each (repeats allowed; overrides --gpus)")
     parser.add_argument("--seed", type=int, default=DEFAULT_SEED, help="sampler seed (counter-based Philox)")
     parser.add_argument("--batch", type=int, default=1 << 18, help="shots per device launch")
     parser.add_argument("--precision", choices=["f32", "f64"], default="f64",
@@ -609,7 +697,7 @@ def p_sweep_main(noise_model_args, noise_model, meas_prior, data_prior):
     result = p_sweep(samples=args.samples, code=code, rounds=args.rounds, noise_model=noise_model,
                      noise_model_args=noise_model_args, meas_prior=meas_prior, data_prior=data_prior,
                      p_values=sweep, decoder_mode=args.decoder_mode, bp_osd_options=bp_osd_options,
-                     gpus=args.gpus, seed=args.seed, batch=args.batch, precision=args.precision,
+                     gpus=args.gpus, devices=args.devices, seed=args.seed, batch=args.batch, precision=args.precision,
                      checkpoint=args.checkpoint)
     result.to_csv(sys.stdout)
     return result

@@ -3,14 +3,40 @@
 Shots are independent, so the only cross-rank traffic is bookkeeping: a
 barrier around the timed region, the max of the per-rank elapsed times and the
 sum of failure / convergence counts -- a few bytes, no data-path collective
-(SURVEY §8(e)).  The Philox sampler is counter-based (key = seed, stream;
-counter = shot index), so shot index ranges fully determine every rank's
-inputs and the union over ranks equals a single-process run over the same
-range.
+(the reference's fan-out is `Pool(cpu_count())` over shots,
+misc/p_sweep.py:17-40, which exchanges only the per-worker failure counts).
+
+Those few bytes live on the host, so the process group is `gloo` on every
+path (GPU ranks and the CPU rehearsal alike) and every collective here takes a
+CPU tensor: the code a CPU test runs is exactly the code an 8-GPU node runs.
+Nothing of the decode crosses ranks, so no RCCL communicator is created.  The
+Philox sampler is counter-based (key = seed, stream; counter = shot index), so
+shot index ranges fully determine every rank's inputs and the union over ranks
+equals a single-process run over the same range.
 """
 from __future__ import annotations
 
-__all__ = ["step_shot0", "shard_range", "reduce_counts", "max_time", "barrier"]
+__all__ = ["BOOKKEEPING_BACKEND", "init_process_group", "rank_device", "step_shot0", "shard_range",
+           "reduce_counts", "max_time", "barrier"]
+
+# the backend of the bookkeeping group: host tensors only (see the module doc)
+BOOKKEEPING_BACKEND = "gloo"
+
+
+def init_process_group(**kw) -> None:
+    """Join the bookkeeping group (env:// rendezvous: RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT, as torchrun sets them)."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group(BOOKKEEPING_BACKEND, **kw)
+
+
+def rank_device(local_rank: int, device_count: int) -> int:
+    """HIP device of a local rank: one GPU per rank; ranks beyond the visible
+    devices share them round-robin (a 1-GPU box can rehearse N ranks)."""
+    if device_count <= 0:
+        raise RuntimeError("no HIP device visible")
+    return int(local_rank) % int(device_count)
 
 
 def step_shot0(step: int, world: int, rank: int, per_rank: int) -> int:
@@ -31,27 +57,39 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
-def reduce_counts(values, device=None):
+def _host(values, dtype):
+    """A CPU tensor of `values` (device tensors are copied to the host first)."""
+    import torch
+    if isinstance(values, torch.Tensor):
+        return values.detach().to("cpu", dtype)
+    return torch.as_tensor(values, dtype=dtype)
+
+
+def reduce_counts(values) -> list:
     """Sum integer counters over ranks (identity when not distributed)."""
     import torch
-    t = torch.as_tensor(values, dtype=torch.int64, device=device)
+    t = _host(values, torch.int64).clone()
     d = _dist()
     if d is not None and d.get_world_size() > 1:
         d.all_reduce(t)
-    return t.cpu().tolist()
+    return t.tolist()
 
 
-def max_time(seconds: float, device=None) -> float:
+def max_time(seconds: float) -> float:
+    """The maximum of `seconds` over ranks."""
     import torch
     d = _dist()
     if d is None or d.get_world_size() == 1:
-        return seconds
-    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+        return float(seconds)
+    t = torch.tensor([float(seconds)], dtype=torch.float64)
     d.all_reduce(t, op=d.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier() -> None:
+    """Host barrier over the bookkeeping group: an all-reduce of one CPU word
+    (dist.barrier() would pick a device by itself)."""
+    import torch
     d = _dist()
     if d is not None and d.get_world_size() > 1:
-        d.barrier()
+        d.all_reduce(torch.zeros(1, dtype=torch.int32))

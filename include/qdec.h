@@ -68,6 +68,16 @@ int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t*
                     int32_t n_data, int32_t fold_blocks, int32_t device, qd_graph** out);
 int qd_graph_destroy(qd_graph* g);
 
+/* Host-only graph: the same validation and host tables as qd_graph_create
+ * (kernel layouts and anneals, flip-set and logical tables, priors) with no
+ * device and no HIP call; the tables are kept in host memory.  For CPU tests
+ * and sanitizer runs (tools/sanitize.sh); decode calls on it fail.
+ * qd_graph_table_digest returns an FNV-1a digest and the byte count of every
+ * table built so far.  No reference counterpart. */
+int qd_graph_create_host(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx, int32_t n_data,
+                         int32_t fold_blocks, qd_graph** out);
+int qd_graph_table_digest(const qd_graph* g, uint64_t* digest, int64_t* bytes);
+
 /* Flip sets for small-set-flip: generator rows (CSR over H's columns; for the
  * storage experiment the X-check rows of Hx).  Each generator must have <= 8
  * qubits whose checks in H number <= 32.  No reference counterpart (SSF is
@@ -191,6 +201,13 @@ int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
  * only 2).  Results are identical at every setting.  No reference counterpart. */
 int qd_graph_set_wave_occupancy(qd_graph* g, int32_t waves_per_cu);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
+
+/* Names of the BP and SSF kernels the last decode call on `g` launched, as
+ * rocprofv3 spells them (template arguments included; "" when a stage did not
+ * run or has no recorded name), NUL-terminated and truncated to the buffer
+ * lengths.  Lets a measurement match a rocprof / PMC entry to the exact
+ * instantiation it timed.  No reference counterpart. */
+int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len);
 
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */

@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libqdec_oracle.so")
+LIB_PATH = os.environ.get("QDEC_ORACLE_LIB") or os.path.join(HERE, "libqdec_oracle.so")  # env: sanitizer variant
 
 _p = C.c_void_p
 _i32 = C.c_int32

@@ -195,3 +195,122 @@ def test_sparse_logicals_accepted_and_copied():
         QuantumCodeLogicals(lz.astype(np.float32), lz)
     d = QuantumCodeLogicals(lz.toarray(), lz.toarray())
     assert not d.x.flags.writeable
+
+
+def test_run_shards_retries_a_failed_shard_once_in_a_fresh_thread():
+    """p_sweep's fan-out (reference misc/p_sweep.py:24-40): a shard that raises
+    is re-run once in a new worker thread on the same device; counters are
+    summed over shards exactly once."""
+    import threading
+
+    from exp_ldpc_amd.experiment import run_shards
+    calls = []
+
+    def work(d, lo, hi, attempt):
+        calls.append((d, lo, hi, attempt, threading.current_thread().name))
+        if d == 1 and attempt == 0:
+            raise RuntimeError("injected shard failure")
+        return [hi - lo, 1, 0.5]
+
+    out = run_shards([(0, 0, 10), (1, 10, 25), (2, 25, 30)], work, p_ph=0.01)
+    assert out == [30, 3, 1.5]
+    first = [c for c in calls if c[3] == 0]
+    retry = [c for c in calls if c[3] == 1]
+    assert len(first) == 3 and [c[:3] for c in retry] == [(1, 10, 25)]
+    assert retry[0][4] != next(c[4] for c in first if c[0] == 1)  # a fresh worker thread
+
+
+def test_run_shards_reports_the_failed_range():
+    from exp_ldpc_amd.experiment import ShardError, run_shards
+
+    def work(d, lo, hi, attempt):
+        if lo == 10:
+            raise ValueError("broken device")
+        return [1]
+
+    with pytest.raises(ShardError) as ei:
+        run_shards([(0, 0, 10), (0, 10, 20)], work, p_ph=0.02)
+    e = ei.value
+    assert (e.p_ph, e.device, e.lo, e.hi) == (0.02, 0, 10, 20) and "shots [10, 20)" in str(e)
+    # one device: the first attempt runs inline, the retry in a thread
+    seen = []
+
+    def once(d, lo, hi, attempt):
+        seen.append(attempt)
+        if attempt == 0:
+            raise RuntimeError("transient")
+        return [hi - lo]
+
+    assert run_shards([(0, 0, 7)], once) == [7] and seen == [0, 1]
+
+
+def test_set_logicals_rejects_1d_dense_input():
+    """A 1-D dense logicals argument is malformed (k x n_data expected); it must
+    not be read as a single logical row.  Checked before any device call."""
+    from exp_ldpc_amd.decoder import Decoder
+    d = Decoder.__new__(Decoder)
+    d.n_data = 5
+    with pytest.raises(ValueError, match="k x n_data"):
+        Decoder.set_logicals(d, np.ones(5, np.uint8))
+
+
+def _host_graph(lib, H, n_data=None, gens=None, lz=None, probs=None):
+    import ctypes as C
+
+    from exp_ldpc_amd import _abi
+    H = sp.csr_matrix(H)
+    H.sort_indices()
+    rp = np.ascontiguousarray(H.indptr, np.int32)
+    ci = np.ascontiguousarray(H.indices, np.int32)
+    h = C.c_void_p()
+    nd = n_data or H.shape[1]
+    _abi.check(lib.qd_graph_create_host(H.shape[0], H.shape[1], _abi.ptr(rp), _abi.ptr(ci), nd, 1, C.byref(h)),
+               "qd_graph_create_host")
+    if gens is not None:
+        G = sp.csr_matrix(gens)
+        G.sort_indices()
+        gp, gi = np.ascontiguousarray(G.indptr, np.int32), np.ascontiguousarray(G.indices, np.int32)
+        _abi.check(lib.qd_graph_set_flipsets(h, G.shape[0], _abi.ptr(gp), _abi.ptr(gi)), "flipsets")
+    if lz is not None:
+        L = sp.csr_matrix(lz)
+        L.sort_indices()
+        lp, li = np.ascontiguousarray(L.indptr, np.int32), np.ascontiguousarray(L.indices, np.int32)
+        _abi.check(lib.qd_graph_set_logicals_csr(h, L.shape[0], _abi.ptr(lp), _abi.ptr(li)), "logicals")
+    if probs is not None:
+        pr = np.ascontiguousarray(np.broadcast_to(np.asarray(probs, np.float64), (H.shape[1],)))
+        _abi.check(lib.qd_graph_set_priors(h, _abi.ptr(pr)), "priors")
+    d, nb = C.c_uint64(0), C.c_int64(0)
+    _abi.check(lib.qd_graph_table_digest(h, C.byref(d), C.byref(nb)), "digest")
+    return h, d.value, nb.value
+
+
+def test_host_only_tables_build_without_a_gpu(code225):
+    """qd_graph_create_host runs the host half of graph setup -- validation,
+    wave-kernel layout anneals (ms_layout), flip-set inverse tables, logicals,
+    priors -- with no device: deterministic tables, and decodes refuse the
+    handle.  tools/sanitize.sh runs this under ASan + UBSan."""
+    import ctypes as C
+
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    hz, hx, lz = code225.checks.z, code225.checks.x, code225.logicals.z
+    h1, d1, b1 = _host_graph(lib, hz, gens=hx, lz=lz, probs=0.01)
+    h2, d2, b2 = _host_graph(lib, hz, gens=hx, lz=lz, probs=0.01)
+    assert d1 == d2 and b1 == b2 and b1 > 10_000
+    h3, d3, _ = _host_graph(lib, hz, gens=hx, lz=lz, probs=0.02)  # other priors: other tables
+    assert d3 != d1
+    prm = _abi.QdParams(50, _abi.QD_MIN_SUM, _abi.QD_F64, 0, 0, 0, 0.0)
+    syn = np.zeros((1, hz.shape[0]), np.uint8)
+    rc = lib.qd_decode_batch(h1, C.byref(prm), 1, _abi.ptr(syn), None, None, None, None, None, None, None, None,
+                             None)
+    assert rc != 0 and b"host-only" in lib.qd_last_error()
+    # ragged random graphs (workgroup-kernel shapes and degree-0 rows/columns)
+    rng = np.random.default_rng(5)
+    for m, n in ((30, 50), (300, 700), (700, 1500)):
+        A = sp.random(m, n, density=4.0 / n, random_state=rng, format="csr")
+        A.data[:] = 1
+        h, d, b = _host_graph(lib, A, probs=rng.uniform(0.001, 0.2, n))
+        assert b > 0
+        lib.qd_graph_destroy(h)
+    for h in (h1, h2, h3):
+        assert lib.qd_graph_destroy(h) == 0

@@ -250,6 +250,39 @@ def test_p_sweep_checkpoint_resume(gpu_available, tmp_path):
     assert list(second["failures"]) == list(fresh["failures"])
 
 
+def test_p_sweep_shards_threads_retry_and_metrics(gpu_available, monkeypatch):
+    """p_sweep's multi-device fan-out on one GPU: three shards (devices [0, 0, 0],
+    one host thread each, ragged ranges) give exactly the failure counts of one
+    shard; a shard whose first attempt raises is retried in a fresh thread with
+    rebuilt handles and the counts stay exact; the row carries the kernel-time
+    metrics (reference fan-out: misc/p_sweep.py:17-40)."""
+    from exp_ldpc_amd import experiment
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    code = load_code("hgp_12_3_4_s1234")
+    opts = {"max_iter": 50, "bp_method": "ms", "ms_scaling_factor": 0, "osd_method": "osd0", "osd_order": 0}
+    prior = lambda p, _, __: 2 * p / 3
+    kw = dict(samples=10001, noise_model=depolarizing_noise, noise_model_args=lambda p: dict(p=p, pm=p),
+              meas_prior=prior, data_prior=prior, code=code, rounds=0, decoder_mode="bpssf", bp_osd_options=opts,
+              seed=9, batch=1024, p_values=[0.02, 0.05])
+    one = experiment.p_sweep(devices=[0], **kw)
+    three = experiment.p_sweep(devices=[0, 0, 0], **kw)
+    assert list(one["failures"]) == list(three["failures"]) and three["gpus"].iloc[0] == 3
+    for col in ("kernel_ms", "hbm_bytes", "hbm_roofline_frac"):
+        assert (three[col] > 0).all()
+    orig_run = experiment.BatchPipeline.run
+    state = {"n": 0}
+
+    def flaky(self, syn, rd, **k):
+        state["n"] += 1
+        if state["n"] == 2:
+            raise RuntimeError("injected shard failure")
+        return orig_run(self, syn, rd, **k)
+
+    monkeypatch.setattr(experiment.BatchPipeline, "run", flaky)
+    retried = experiment.p_sweep(devices=[0, 0], **kw)
+    assert list(retried["failures"]) == list(one["failures"])
+
+
 def _raw_history(syn, R, m):
     """Undo the spacetime differencing (spacetime_code.py:98-119): s_t = xor of sigma_0..sigma_t."""
     sv = syn.reshape(syn.shape[0], R + 1, m)
