@@ -550,7 +550,7 @@ def main():
             bp_ms[:, pi] = a[:args.iso_steps]
             ssf_ms[:, pi] = c[:args.iso_steps]
         it_iso = run.iters[args.warmup:args.warmup + args.iso_steps].to(torch.int64).sum(dim=2).cpu().numpy()
-        names = ("", "") if fake else dset[-1].last_kernels()  # the instantiations the isolated phase ran
+        names = ("", "", "") if fake else dset[-1].last_kernels()  # the instantiations the isolated phase ran
         iso[prec] = (bp_ms, ssf_ms, it_iso, names)
 
     # ---- phase 4: sampling + decode in the timed region ----
@@ -593,8 +593,11 @@ def main():
                 row[variant[0]] = vr
             ler[key] = row
 
-        bp_ms, ssf_ms, it_iso, (bp_kernel, ssf_kernel) = iso[args.precision]
+        bp_ms, ssf_ms, it_iso, (bp_kernel, ssf_kernel, pre_kernel) = iso[args.precision]
         roof = lds_roofline(bp_ms, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms)
+        if pre_kernel:
+            roof["pre_kernel"] = pre_kernel
+            roof["timing"] += f"; the BP launch time includes its shot-triage pass {pre_kernel}"
         pmc = None if fake else pmc_ceilings(bp_kernel)
         if pmc is not None:
             src, name, k = pmc

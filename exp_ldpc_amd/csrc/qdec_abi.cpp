@@ -119,7 +119,7 @@ struct qd_graph {
     hipEvent_t ssf_ev = nullptr;
     hipStream_t ws_last = nullptr;
     // kernels the last decode on this handle launched (qd_graph_last_kernels)
-    std::string last_bp, last_ssf;
+    std::string last_bp, last_ssf, last_pre;
     // qd_graph_create_host: tables only, no device, no stream; decodes refuse it
     bool host_only = false;
 };
@@ -673,20 +673,29 @@ void build_tables(qd_graph* G, int m, int n) {
 }
 
 // Attach the SSF queue scratch (capacity >= B shots) to the launch arguments.
+// Words of a compact-list entry (wave graphs; qdec_bp_ms.h CmpEntry): shot,
+// syndrome words, readout logical-parity words.
+size_t cmp_entry_bytes(const DevGraph& g) { return 8 * (1 + (size_t)g.m_pad / 64 + 4); }
+
+// Attach the SSF queue scratch (capacity >= B shots) and, for wave graphs, the
+// compact shot list of lean launches to the launch arguments.
 void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
-    if (a.B <= 0 || (!a.ssf && !lds_kernel_applies(G->dg, method, precision, a)))
-        return;
     const DevGraph& g = G->dg;
+    const bool cmp = g.wave && method == QD_MIN_SUM && !G->ms_var_of_slot.empty();
+    if (a.B <= 0 || (!a.ssf && !cmp && !lds_kernel_applies(G->dg, method, precision, a)))
+        return;
     if (a.B > G->q_cap) {
         ws_drain(G);  // launches still in flight may use the old queue
         if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
         G->qws = nullptr;
         G->q_cap = 0;
         // byte format: idx[B] | x[B][n] | r[B][m]; packed format (wave kernels) reuses
-        // the x region for [B][1 + 2 n_pad/64 + m_pad/64] u64 entries
+        // the x region for [B][1 + 2 n_pad/64 + m_pad/64] u64 entries; then the
+        // compact list [B] entries (wave graphs)
         const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
         const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
-        const size_t bytes = 256 + (size_t)a.B * (8 + xr) + 256;
+        const size_t cl = g.wave ? cmp_entry_bytes(g) : 0;
+        const size_t bytes = 256 + (size_t)a.B * (8 + xr) + 256 + (size_t)a.B * cl + 256;
         hip_check(hipMalloc(&G->qws, bytes), "hipMalloc queue");
         G->q_cap = a.B;
     }
@@ -696,6 +705,12 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
     a.q_x = base + 256 + (size_t)G->q_cap * 8;
     a.q_r = a.q_x + (size_t)G->q_cap * g.n;
     a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
+    if (g.wave) {
+        const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
+        const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
+        a.cmp = reinterpret_cast<uint64_t*>(base + 256 + (size_t)G->q_cap * (8 + xr) + 256);
+        a.cmp_count = a.wave_ctr ? a.wave_ctr + 2 : nullptr;
+    }
 }
 
 void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& a, size_t* bytes) {
@@ -729,6 +744,7 @@ void note_kernels(qd_graph* G) {
     const LaunchNames& n = last_launch_names();
     G->last_bp = n.bp ? n.bp : "";
     G->last_ssf = n.ssf ? n.ssf : "";
+    G->last_pre = n.pre ? n.pre : "";
 }
 
 void attach_timing(qd_graph* G, DecodeArgs& a) {
@@ -1043,6 +1059,7 @@ static void upload_logicals(qd_graph* G, int32_t k, std::vector<int32_t> ptr, st
     G->lz_arena.release();
     g.lz = nullptr;
     g.lz_ptr = g.lz_idx = nullptr;
+    g.ms_lzs = nullptr;
     g.k = 0;
     g.lz_sparse = 0;
     if (k == 0) return;
@@ -1068,6 +1085,25 @@ static void upload_logicals(qd_graph* G, int32_t k, std::vector<int32_t> ptr, st
     }
     g.lz_ptr = G->lz_arena.upload(cptr);
     g.lz_idx = G->lz_arena.upload(cidx);
+    // wave graphs: the same logicals in the min-sum kernel's lane-slot order
+    // ([k][n_pad/64] words, bit s%64 of word s/64 = the column of slot s), so the
+    // compact-list kernel tests its ballot words without a column permutation
+    g.ms_lzs = nullptr;
+    if (!G->ms_var_of_slot.empty() && k <= 256) {
+        const int RVn = g.n_pad / 64;
+        std::vector<int> col_bit(g.n_data, -1);
+        for (int sl = 0; sl < g.n_pad; ++sl) {
+            const int j = G->ms_var_of_slot[sl];
+            if (j >= 0 && j < g.n_data) col_bit[j] = sl;
+        }
+        std::vector<uint64_t> lzs((size_t)k * RVn, 0);
+        for (int r = 0; r < k; ++r)
+            for (int t = cptr[r]; t < cptr[r + 1]; ++t) {
+                const int sl = col_bit[cidx[t]];
+                if (sl >= 0) lzs[(size_t)r * RVn + sl / 64] |= 1ull << (sl % 64);
+            }
+        g.ms_lzs = G->lz_arena.upload(lzs);
+    }
     // a support walk costs ~ one gather per entry, the dense test one word per
     // (logical, word): walk when that is clearly cheaper, or when there is no table
     g.lz_sparse = (!g.lz || cidx.size() <= (size_t)k * W / 4) ? 1 : 0;
@@ -1383,7 +1419,8 @@ int qd_graph_read_timing(qd_graph* G, float* bp_ms, float* ssf_ms, int32_t max_c
     });
 }
 
-int qd_graph_last_kernels(qd_graph* G, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len) {
+int qd_graph_last_kernels(qd_graph* G, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len, char* pre,
+                          int32_t pre_len) {
     return guarded([&] {
         check_graph(G);
         auto put = [](const std::string& v, char* out, int32_t len) {
@@ -1394,6 +1431,7 @@ int qd_graph_last_kernels(qd_graph* G, char* bp, int32_t bp_len, char* ssf, int3
         };
         put(G->last_bp, bp, bp_len);
         put(G->last_ssf, ssf, ssf_len);
+        put(G->last_pre, pre, pre_len);
     });
 }
 

@@ -637,15 +637,20 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             if (want_fail) {  // readout words came with the queue entry
                 // the readout words are re-read from this slot's staging buffer
                 // (restaged only by the next slot), not held across the steps
+                // (q_rpar: the entry holds the readout's logical parities, bit r
+                // of word r / 64, instead of the readout words)
+                const bool rpar = a.q_rpar != 0;
                 uint64_t Rd[XW];
 #pragma unroll
-                for (int w = 0; w < XW; ++w) Rd[w] = __ballot(xh[w * 64 + lane] & 1) ^ ew[1 + XW + RW + w];
+                for (int w = 0; w < XW; ++w) Rd[w] = __ballot(xh[w * 64 + lane] & 1) ^ (rpar ? 0ull : ew[1 + XW + RW + w]);
                 QDEC_STAMP(8);
                 int f = 0;
 #pragma unroll
                 for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
                     const int r = rr * 64 + lane;
-                    if (r < g.k) f |= lz_row_parity<XW>(g, lzs, r, Rd);
+                    if (r < g.k)
+                        f |= lz_row_parity<XW>(g, lzs, r, Rd) ^
+                             (rpar && rr < XW ? (int)((ew[1 + XW + RW + (rr < XW ? rr : 0)] >> lane) & 1) : 0);
                 }
                 any_fail = __ballot(f) != 0ull;
                 QDEC_STAMP(9);
@@ -735,6 +740,30 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
 
 // BP kernel of a wave shape: min-sum uses the compressed-state kernel, product-sum
 // the message-array kernel.
+// Lean launches: no x / corr / llr outputs, no base, no syndrome flags, no fold.
+static bool lean_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
+    return !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1 &&
+           (!defer || a.q_packed);
+}
+
+// The two-pass compact path (ms_triage_kernel + bp_ms_cmp_kernel) serves lean
+// min-sum launches whose graph has the slot-order logicals (or no fused check);
+// QDEC_COMPACT=0 keeps the one-pass kernel (A/B, parity tests run both).
+static bool compact_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
+    const char* v = std::getenv("QDEC_COMPACT");  // read per launch: tests switch it within a process
+    const bool off = v && v[0] == '0';
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    return !off && a.cmp && a.cmp_count && a.syn && lean_launch(g, a, defer) && (!want_fail || g.ms_lzs);
+}
+
+template <int RC, int RV>
+static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t stream) {
+    const size_t lds = 4 * (size_t)(((int64_t)64 * g.m + 3) / 4 + 2 + ((int64_t)64 * g.n_data + 3) / 4 + 2);
+    QDEC_NOTE_PRE("qdec::ms_triage_kernel", RC, RV);
+    hipLaunchKernelGGL((ms_triage_kernel<RC, RV>), dim3((unsigned)((a.B + 63) / 64)), dim3(64), lds, stream, g, a);
+    return (int)hipGetLastError();
+}
+
 template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
 static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if constexpr (METHOD == 1) {
@@ -746,12 +775,38 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             const hipError_t e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);
             if (e != hipSuccess) return (int)e;
         }
-        const bool lean = !a.x_out && !a.corr_out && !a.llr_out && !a.base && !a.syn_flags && g.fold_blocks == 1 &&
-                          (!DEFER || a.q_packed);
+        const bool lean = lean_launch(g, a, DEFER);
         // f64: 2 waves per SIMD measured faster than 3 for a lone decode at every
         // p (n = 225: 7.1 vs 9.3 ms per 2^18 shots at p = 0.1); concurrent
         // decodes may ask for more (qd_graph_set_wave_occupancy)
         const int cap = g.wave_occ > 0 ? g.wave_occ : (sizeof(T) == 8 ? 8 : 0);
+        if (a.q_rpar || (!DEFER && compact_launch(g, a, DEFER))) {  // two passes: triage, then the listed shots
+            DecodeArgs b = a;
+            b.cmp_zero_ok = (g.ms_allpos >> (sizeof(T) == 4 ? 1 : 0)) & 1;
+            hipError_t e = hipMemsetAsync(b.cmp_count, 0, sizeof(unsigned long long), stream);
+            if (e != hipSuccess) return (int)e;
+            int rc = launch_triage<RC, RV>(g, b, stream);
+            if (rc != 0) return rc;
+            const size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16;
+            // degree-3 rounds: the (2, 4, 7) shape instantiates D3R = 2 (n = 225 HGP: 144 degree-3 columns)
+            if constexpr (RC == 2 && RV == 4 && DRC == 7) {
+                if (g.ms_d3r >= 2) {
+                    if constexpr (sizeof(T) == 8) {
+                        if (cap > 8) {  // 3 waves per SIMD
+                            QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 2, 3);
+                            return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 2, 3>, clds, b.B,
+                                                     num_cus, stream, g, b, 64, cap);
+                        }
+                    }
+                    QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 2, 0);
+                    return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 2>, clds, b.B, num_cus, stream,
+                                             g, b, 64, cap);
+                }
+            }
+            QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 0, 0);
+            return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 0>, clds, b.B, num_cus, stream, g, b, 64,
+                                     cap);
+        }
         // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
             if (g.ms_d3r >= 2) {
@@ -794,6 +849,9 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hip
     const bool ssf_wave = g.n_gen <= 128 && g.g_lc8;
     a.q_packed = a.ssf && ssf_wave ? 1 : 0;
     a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
+    // compact path with SSF: the queue entries carry readout parities
+    // (the entry's readout area holds RV words: up to 64 RV logicals)
+    a.q_rpar = (METHOD == 1 && a.ssf && ssf_wave && g.k <= 64 * RV && compact_launch(g, a, true)) ? 1 : 0;
     if (!a.ssf) {
         record_ev(a, 0, stream);
         const int rc = launch_bp_wave<T, METHOD, RC, RV, DRC, false>(g, a, num_cus, stream);

@@ -724,4 +724,256 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     QDEC_FLUSH_AT(0);
 }
 
+// ---------------------------------------------------------------- compact shot list
+// Lean min-sum launches on wave graphs run in two passes.  ms_triage_kernel
+// streams every shot's syndrome and readout rows once (coalesced tiles of 64
+// shots), packs the syndrome into bit words and reduces the readout to its
+// logical parities (bit r = parity of Lz[r] . readout).  A shot with an
+// all-zero syndrome under all-positive priors converges in iteration 1 with
+// x = 0 (every message >= 0, so every posterior >= its prior > 0: the same
+// shortcut the one-pass kernel takes), so its outputs are written right there
+// (iterations 1, status 3, no SSF steps, failure = any readout parity).  Every
+// other shot is appended to a compact list: shot index, syndrome words,
+// readout-parity words.  bp_ms_cmp_kernel then decodes only the listed shots,
+// reading each as one entry from registers (no row staging, no readout): its
+// failure check is the parity of Lz (in lane-slot order, ms_lzs) against the
+// ballot words of the hard decision, XOR the readout parities, and a
+// BP-failed shot enters the SSF queue with the parities in place of the
+// readout words (q_rpar), which the SSF kernel's check uses the same way.
+template <int RC>
+struct CmpEntry {
+    static constexpr int EW = 1 + RC + kMaxLogicalRounds;  // shot, syndrome words, readout-parity words
+    static constexpr int kPer = 4;                          // entries per chunk (one u64 load per lane)
+    static_assert(kPer * EW <= 64, "chunk");
+};
+
+// bits 24..27 of (d & 0x01010101) * 0x01020408 are bit 0 of d's four bytes
+__device__ __forceinline__ uint32_t byte_bits4(uint32_t d) { return ((d & 0x01010101u) * 0x01020408u) >> 24; }
+
+// Copy bytes [start, start + len) of a buffer of `total` bytes into LDS as the
+// dwords covering them (dst[0] = the dword at or below `start`); returns the
+// byte offset of `start` inside dst.  Coalesced: 64 lanes x 8 dwords per round,
+// all loads of a round issued before any LDS store.  Dwords past the buffer's
+// last whole dword are assembled from byte loads.
+__device__ __forceinline__ int tile_to_lds(const uint8_t* buf, int64_t total, int64_t start, int64_t len,
+                                           uint32_t* dst, int lane) {
+    const int64_t d0 = start >> 2;
+    const int nd = (int)(((start + len + 3) >> 2) - d0);
+    const int64_t whole = total >> 2;  // dwords fully inside the buffer
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(buf) + d0;
+    constexpr int U = 8;
+    for (int b = 0; b < nd; b += 64 * U) {
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int d = b + u * 64 + lane;
+            v[u] = (d < nd && d0 + d < whole) ? __builtin_nontemporal_load(src + d) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int d = b + u * 64 + lane;
+            if (d < nd) {
+                uint32_t w = v[u];
+                if (d0 + d >= whole) {  // the buffer's last 1-3 bytes
+                    w = 0u;
+                    for (int t = 0; t < 4; ++t) {
+                        const int64_t q = 4 * (d0 + d) + t;
+                        if (q < total) w |= (uint32_t)buf[q] << (8 * t);
+                    }
+                }
+                dst[d] = w;
+            }
+        }
+    }
+    return (int)(start & 3);
+}
+
+// NB bytes of a lane's row at byte offset `off` of an LDS dword image, as bit
+// words (bit i of word i/64 = bit 0 of byte i); bytes >= len are cleared.
+template <int NW>
+__device__ __forceinline__ void row_bits(const uint32_t* img, int off, int len, uint64_t (&w)[NW]) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = 0ull;
+    const int q = off >> 2, sh = off & 3;
+    uint32_t lo = img[q];
+#pragma unroll
+    for (int t = 0; t < 16 * NW; ++t) {
+        if (4 * t < len) {
+            const uint32_t hi = img[q + t + 1];
+            // the 4 bytes at off + 4t: ({hi, lo} >> 8 sh)[31:0]
+            uint32_t nib = byte_bits4(__builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh));
+            lo = hi;
+            if (4 * t + 4 > len) nib &= (1u << (len - 4 * t)) - 1u;
+            w[t / 16] |= (uint64_t)nib << (4 * (t % 16));
+        }
+    }
+}
+
+// One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).
+template <int RC, int NWD>
+__global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
+    using Ent = CmpEntry<RC>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const int m = g.m, nd = g.n_data;
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
+    const int ns = (int)min((int64_t)64, a.B - s0);
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    uint32_t* syn_img = reinterpret_cast<uint32_t*>(smem);
+    const int syn_dw = (64 * m + 3) / 4 + 2;
+    uint32_t* rd_img = syn_img + syn_dw;
+    const int ssh = tile_to_lds(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img, lane);
+    const int rsh = want_fail ? tile_to_lds(a.readout, a.B * (int64_t)nd, s0 * nd, (int64_t)ns * nd, rd_img, lane) : 0;
+    __syncthreads();
+    const bool live = lane < ns;
+    const int64_t shot = s0 + lane;
+    uint64_t sw[RC];
+    row_bits<RC>(syn_img, ssh + lane * m, m, sw);
+    uint64_t rp[kMaxLogicalRounds] = {0ull, 0ull, 0ull, 0ull};
+    if (want_fail) {
+        uint64_t rw[NWD];
+        row_bits<NWD>(rd_img, rsh + lane * nd, nd, rw);
+        for (int r = 0; r < g.k; ++r) {  // uniform rows of the dense logical table
+            int par = 0;
+#pragma unroll
+            for (int w = 0; w < NWD; ++w)
+                if (w < g.lz_words) par += __popcll(g.lz[(size_t)r * g.lz_words + w] & rw[w]);
+#pragma unroll
+            for (int rr = 0; rr < kMaxLogicalRounds; ++rr)
+                if (rr == (r >> 6)) rp[rr] |= (uint64_t)(par & 1) << (r & 63);
+        }
+    }
+    uint64_t any = 0ull;
+#pragma unroll
+    for (int rc = 0; rc < RC; ++rc) any |= sw[rc];
+    const bool trivial = live && any == 0ull && a.cmp_zero_ok;
+    if (live && trivial) {
+        if (a.iters) a.iters[shot] = 1;
+        if (a.status) a.status[shot] = 3;
+        if (a.ssf_steps) a.ssf_steps[shot] = 0;
+        if (a.fail) a.fail[shot] = (uint8_t)((rp[0] | rp[1] | rp[2] | rp[3]) != 0ull);
+    }
+    const bool listed = live && !trivial;
+    const unsigned long long bal = __ballot(listed);
+    if (bal == 0ull) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(a.cmp_count, (unsigned long long)__popcll(bal));
+    base = __shfl(base, 0);
+    if (listed) {
+        const uint64_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        uint64_t* e = a.cmp + (base + rank) * Ent::EW;
+        e[0] = (uint64_t)shot;
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) e[1 + rc] = sw[rc];
+#pragma unroll
+        for (int rr = 0; rr < kMaxLogicalRounds; ++rr) e[1 + RC + rr] = rp[rr];
+    }
+}
+
+// v_readlane of a 64-bit value (lane uniform)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// The compact-list BP kernel (see above): the lean bp_ms_wave_kernel's BP
+// (MsCore) on the listed shots only.  Entries come in chunks of CmpEntry::kPer
+// (one u64 per lane, the next chunk loaded while this one decodes); chunks are
+// handed out by ShotSeq (static stride, then a counter for the tail).
+template <typename T, int RC, int RV, int DRC, bool DEFER, int D3R, int OCC = 0>
+__global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void bp_ms_cmp_kernel(DevGraph g, DecodeArgs a) {
+    using Core = MsCore<T, RC, RV, DRC, true, D3R>;
+    using Ent = CmpEntry<RC>;
+    constexpr int EW = Ent::EW, KP = Ent::kPer;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* v2c = reinterpret_cast<T*>(smem);
+    T* st = v2c + MsLds<T>::v2c_elems(MsLds<T>::rows(g));
+    uint8_t* xh = reinterpret_cast<uint8_t*>(st + MsLds<T>::state_elems(g.m_pad));
+    uint64_t* lzs = reinterpret_cast<uint64_t*>(smem + MsLds<T>::core_bytes(g));  // [k][RV] slot-order logicals
+
+    const int lane = threadIdx.x;
+    const int m = g.m;
+    Core core;
+    core.load(g, lane);
+    Core::init_lds(g, v2c, st, xh, lane);
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    if (want_fail)
+        for (int e = lane; e < g.k * RV; e += 64) lzs[e] = g.ms_lzs[e];
+    wave_lds_sync();
+
+    const int64_t count = (int64_t)*a.cmp_count;
+    const int64_t nch = (count + KP - 1) / KP;
+    // the chunk counter only pays when the tail is long (>= 16 chunks per wave)
+    unsigned long long* ctr = a.wave_ctr && nch >= 16 * (int64_t)gridDim.x ? a.wave_ctr : nullptr;
+    ShotSeq seq(nch, ctr, blockIdx.x, gridDim.x, lane, 1);
+    auto load_chunk = [&](int64_t c) -> uint64_t {
+        const int64_t e = c * (KP * EW) + lane;
+        return (c < nch && lane < KP * EW && e < count * EW) ? __builtin_nontemporal_load(a.cmp + e) : 0ull;
+    };
+    int64_t c = seq.next(lane);
+    uint64_t ent = load_chunk(c);
+    while (c < nch) {
+        const int64_t cn = seq.next(lane);
+        const uint64_t entn = load_chunk(cn);
+        const int ne = (int)min((int64_t)KP, count - c * KP);
+        for (int q = 0; q < ne; ++q) {
+            const int64_t shot = (int64_t)readlane64(ent, q * EW);
+            bool sbit[RC];
+#pragma unroll
+            for (int rc = 0; rc < RC; ++rc) sbit[rc] = (readlane64(ent, q * EW + 1 + rc) >> lane) & 1;
+            uint64_t rpar[kMaxLogicalRounds];
+#pragma unroll
+            for (int rr = 0; rr < kMaxLogicalRounds; ++rr) rpar[rr] = readlane64(ent, q * EW + 1 + RC + rr);
+            core.write_priors(v2c);
+            wave_lds_sync();
+            T Q[RV];
+            uint64_t X[RV];
+            bool pres[RC];
+            int it = 1;
+            const bool conv = core.iterate(a, v2c, st, m, lane, sbit, Q, X, pres, it);
+            const int iters = conv ? it : a.max_iter;
+            if (lane == 0 && a.iters) a.iters[shot] = iters;
+            if (DEFER && !conv) {
+                // hard decision by column for the SSF queue (slot order -> xh[column])
+#pragma unroll
+                for (int rv = 0; rv < RV; ++rv) xh[core.col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
+                wave_lds_sync();
+                uint64_t xw[RV], rw[RC], dw[RV];
+#pragma unroll
+                for (int w = 0; w < RV; ++w) {
+                    xw[w] = __ballot(xh[w * 64 + lane] & 1);
+                    dw[w] = w < kMaxLogicalRounds ? rpar[w < kMaxLogicalRounds ? w : 0] : 0ull;
+                }
+#pragma unroll
+                for (int rc = 0; rc < RC; ++rc) rw[rc] = __ballot(pres[rc]);
+                queue_push_packed<RV, RC>(a, shot, xw, rw, dw, lane);
+                wave_lds_sync();
+            } else {
+                int f = 0;
+                if (want_fail) {  // parity of Lz x (slot order) against the readout's
+#pragma unroll
+                    for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                        const int r = rr * 64 + lane;
+                        if (r < g.k) {
+                            int par = (int)((rpar[rr] >> lane) & 1);
+#pragma unroll
+                            for (int w = 0; w < RV; ++w) par += __popcll(lz_word(lzs, (size_t)r * RV + w) & X[w]);
+                            f |= par & 1;
+                        }
+                    }
+                }
+                const int any_fail = __ballot(f) != 0ull;
+                if (lane == 0) {
+                    if (a.status) a.status[shot] = (uint8_t)(conv ? 3 : 0);
+                    if (a.ssf_steps) a.ssf_steps[shot] = 0;
+                    if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+                }
+            }
+        }
+        c = cn;
+        ent = entn;
+    }
+}
+
 }  // namespace qdec

@@ -114,6 +114,7 @@ struct DevGraph {
     // logicals (fused failure check)
     int k, lz_words;
     const uint64_t* lz;           // [k][lz_words]    bit q%64 of word q/64 (nullptr when too large)
+    const uint64_t* ms_lzs;       // wave graphs: [k][n_pad/64] the same by min-sum lane slot (ms_vslot order)
     // the same logicals as CSR supports over data qubits (always set with k > 0);
     // lz_sparse: the workgroup finalize tests logicals on their supports (nnz small
     // against k * lz_words) instead of by dense words
@@ -164,6 +165,15 @@ struct DecodeArgs {
     // optional timing (host side only): events recorded on the launch stream
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr
+    // compact shot list of lean min-sum wave launches (ms_triage_kernel ->
+    // bp_ms_cmp_kernel): entries [B][CmpEntry::EW] u64, count at cmp_count
+    // (zeroed by the launcher); nullptr -> no compact path
+    uint64_t* cmp;
+    unsigned long long* cmp_count;
+    int cmp_zero_ok;  // every prior of the launch's precision > 0: zero syndromes finish in the triage
+    // packed SSF queue entries carry the readout's logical parities (bit r of
+    // the dw area = parity of Lz[r] . readout) instead of the readout words
+    int q_rpar;
 };
 
 // Arguments of the GPU OSD stage (qdec_osd.hip).  Shots whose status has bit 0
@@ -194,6 +204,7 @@ inline void record_ev(const DecodeArgs& a, int i, hipStream_t s) {
 struct LaunchNames {
     const char* bp = "";
     const char* ssf = "";
+    const char* pre = "";  // a pass before the BP kernel (ms_triage_kernel), inside the BP timing
 };
 LaunchNames& last_launch_names();
 
@@ -215,6 +226,11 @@ inline std::string kernel_name(const char* base, A... args) {
     do {                                                            \
         static const std::string qdec_kn_ = kernel_name(__VA_ARGS__); \
         last_launch_names().bp = qdec_kn_.c_str();                  \
+    } while (0)
+#define QDEC_NOTE_PRE(...)                                          \
+    do {                                                            \
+        static const std::string qdec_kn_ = kernel_name(__VA_ARGS__); \
+        last_launch_names().pre = qdec_kn_.c_str();                 \
     } while (0)
 #define QDEC_NOTE_SSF(...)                                          \
     do {                                                            \

@@ -285,13 +285,15 @@ class Decoder:
                    "qd_graph_read_timing")
         return bp[:cnt.value].astype(np.float64), ssf[:cnt.value].astype(np.float64)
 
-    def last_kernels(self) -> tuple[str, str]:
-        """(BP kernel, SSF kernel) the last decode call launched, in rocprofv3's
-        spelling with template arguments ("" for a stage that did not run)."""
-        bp = C.create_string_buffer(512)
-        ssf = C.create_string_buffer(512)
-        _abi.check(self._lib.qd_graph_last_kernels(self._handle, bp, 512, ssf, 512), "qd_graph_last_kernels")
-        return bp.value.decode(), ssf.value.decode()
+    def last_kernels(self) -> tuple[str, str, str]:
+        """(BP kernel, SSF kernel, pre-pass) the last decode call launched, in
+        rocprofv3's spelling with template arguments ("" for a stage that did
+        not run); the pre-pass (lean launches' shot triage) runs inside the BP
+        timing."""
+        bp, ssf, pre = (C.create_string_buffer(512) for _ in range(3))
+        _abi.check(self._lib.qd_graph_last_kernels(self._handle, bp, 512, ssf, 512, pre, 512),
+                   "qd_graph_last_kernels")
+        return bp.value.decode(), ssf.value.decode(), pre.value.decode()
 
     def close(self) -> None:
         if getattr(self, "_handle", None) and self._handle.value:

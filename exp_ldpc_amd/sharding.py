@@ -25,10 +25,30 @@ BOOKKEEPING_BACKEND = "gloo"
 
 def init_process_group(**kw) -> None:
     """Join the bookkeeping group (env:// rendezvous: RANK / WORLD_SIZE /
-    MASTER_ADDR / MASTER_PORT, as torchrun sets them)."""
+    MASTER_ADDR / MASTER_PORT, as torchrun sets them).  Gloo announces its
+    connections on the process's stdout (C++ printf), which would land beside
+    rank 0's one JSON line, so stdout is pointed at stderr while it connects."""
+    import os
+    import sys
+
     import torch.distributed as dist
-    if not dist.is_initialized():
+    if dist.is_initialized():
+        return
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
         dist.init_process_group(BOOKKEEPING_BACKEND, **kw)
+        barrier()  # every pair connected before stdout is restored
+    finally:
+        sys.stdout.flush()
+        try:  # C stdio buffers too (the announcements are C++ prints)
+            import ctypes
+            ctypes.CDLL(None).fflush(None)
+        except Exception:
+            pass
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def rank_device(local_rank: int, device_count: int) -> int:

@@ -202,12 +202,14 @@ int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
 int qd_graph_set_wave_occupancy(qd_graph* g, int32_t waves_per_cu);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
 
-/* Names of the BP and SSF kernels the last decode call on `g` launched, as
- * rocprofv3 spells them (template arguments included; "" when a stage did not
- * run or has no recorded name), NUL-terminated and truncated to the buffer
- * lengths.  Lets a measurement match a rocprof / PMC entry to the exact
- * instantiation it timed.  No reference counterpart. */
-int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len);
+/* Names of the BP and SSF kernels the last decode call on `g` launched, and of
+ * the pass run before the BP kernel inside the BP timing (the lean launches'
+ * shot triage), as rocprofv3 spells them (template arguments included; "" when
+ * a stage did not run or has no recorded name), NUL-terminated and truncated to
+ * the buffer lengths.  Lets a measurement match a rocprof / PMC entry to the
+ * exact instantiation it timed.  No reference counterpart. */
+int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len, char* pre,
+                          int32_t pre_len);
 
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */

@@ -19,8 +19,8 @@ def test_bench_gpus2_self_launches_two_ranks_and_merges():
                           "--batch", "1000", "--steps", "2", "--points", "3", "--no-cpu-baseline"],
                          capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out.stdout[-2000:]  # rank 0 prints exactly one line
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout[-2000:]  # stdout: rank 0's one JSON line only
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["scaling"] == "weak"
     assert r["config"]["global_batch"] == 1000 * 3 * 2

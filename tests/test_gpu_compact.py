@@ -1,0 +1,130 @@
+"""The compact-list path of lean min-sum launches (ms_triage_kernel +
+bp_ms_cmp_kernel, qdec_bp_ms.h) against the oracle on the edges the bench
+shapes do not reach: every wave shape, batch sizes around the 64-shot triage
+tile and the 4-entry chunks, syndrome / readout buffers whose byte length is
+not a multiple of 4, more than 64 logicals (several readout-parity words),
+no fused check, partial outputs, zero-syndrome shots with and without positive
+priors, and the SSF queue carrying readout parities.  Every output equals the
+oracle's; the one-pass kernel (QDEC_COMPACT=0) gives the same bytes."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import load_checks, load_code
+
+pytestmark = pytest.mark.gpu
+
+OUTS = (("iters", "int32"), ("status", "uint8"), ("ssf_steps", "int32"), ("fail", "uint8"))
+
+
+def _decode_device(dec, syn, rd, keys=("iters", "status", "ssf_steps", "fail")):
+    import torch
+    dev = torch.device("cuda", 0)
+    B = syn.shape[0]
+    out = {k: torch.full((B,), 77, dtype=getattr(torch, dt), device=dev) for k, dt in OUTS if k in keys}
+    dec.decode_device(B, syn=torch.from_numpy(np.ascontiguousarray(syn)).to(dev),
+                      readout=None if rd is None else torch.from_numpy(np.ascontiguousarray(rd)).to(dev), **out)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}, dec.last_kernels()
+
+
+def _random_graph(rng, m, n, dmax=7, cmax=4):
+    from exp_ldpc_amd.codes import make_check_matrix
+    rows, colcount = [], np.zeros(n, int)
+    for _ in range(m):
+        d = int(rng.integers(1, dmax + 1))
+        cand = [j for j in rng.permutation(n) if colcount[j] < cmax][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    return make_check_matrix(rows, n)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("mn", [(40, 90), (110, 170), (120, 230), (100, 370), (200, 520)])
+def test_compact_every_wave_shape(gpu_available, oracle_lib, precision, mn, monkeypatch):
+    """Random ragged graphs that land on each wave shape; odd m, n (row bytes not
+    a multiple of 4); batch sizes 1, 63, 65, 4099; random logicals (k = 3, 70,
+    130: one to three parity words); BP only (no SSF)."""
+    from exp_ldpc_amd.decoder import Decoder
+    m, n = mn
+    rng = np.random.default_rng(m * 1000 + n)
+    H = _random_graph(rng, m, n)
+    probs = rng.uniform(0.005, 0.05, n)
+    for k in (3, 70, 130):
+        L = (rng.random((k, n)) < 0.05).astype(np.uint8)
+        dec = Decoder(H, probs, method="ms", precision=precision, max_iter=20, logicals=L)
+        for B in (1, 63, 65, 4099):
+            e = (rng.random((B, n)) < 0.02).astype(np.uint8)
+            e[: B // 3] = 0
+            syn = ((H @ e.T).T % 2).astype(np.uint8)
+            rd = (e ^ (rng.random((B, n)) < 0.01)).astype(np.uint8)
+            got, (bp_k, _, pre_k) = _decode_device(dec, syn, rd)
+            assert "cmp_kernel" in bp_k and "triage" in pre_k, bp_k
+            ref = oracle_lib.decode(H, probs, syn, method="ms", precision=precision, max_iter=20, lz=L, readout=rd,
+                                    want_llr=False)
+            for key in got:
+                assert np.array_equal(got[key], ref[key]), (k, B, key)
+            monkeypatch.setenv("QDEC_COMPACT", "0")
+            one, (bp1, _, _) = _decode_device(dec, syn, rd)
+            monkeypatch.delenv("QDEC_COMPACT")
+            assert "bp_ms_wave_kernel" in bp1
+            for key in got:
+                assert np.array_equal(one[key], got[key]), (k, B, key)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_compact_ssf_rpar_and_partial_outputs(gpu_available, oracle_lib, precision, code225):
+    """BP + SSF on the n = 225 code with logicals of 1, 2 and 3 parity words
+    (the code's 9 plus random rows): the SSF queue carries readout parities;
+    outputs requested in subsets; no readout (no fused check: fail = 0)."""
+    from exp_ldpc_amd.decoder import Decoder
+    hx, hz = load_checks("hgp_12_3_4_s1234")
+    rng = np.random.default_rng(44)
+    n = hz.shape[1]
+    B = 3001
+    e = (rng.random((B, n)) < 0.04).astype(np.uint8)
+    e[::7] = 0
+    syn = ((hz @ e.T).T % 2).astype(np.uint8)
+    rd = (e ^ (rng.random((B, n)) < 0.003)).astype(np.uint8)
+    lz9 = code225.logicals.z.toarray() % 2 if sp.issparse(code225.logicals.z) else np.asarray(code225.logicals.z)
+    for extra in (0, 60, 140):
+        L = np.vstack([lz9, (rng.random((extra, n)) < 0.03).astype(np.uint8)])
+        dec = Decoder(hz, 0.027, method="ms", precision=precision, max_iter=30, flip_sets=hx, logicals=L)
+        ref = oracle_lib.decode(hz, 0.027, syn, method="ms", precision=precision, max_iter=30, ssf=True, gens=hx, lz=L,
+                                readout=rd, want_llr=False, ssf_impl="fast")
+        assert ref["ssf_steps"].sum() > 0 and ref["fail"].any()
+        got, (bp_k, ssf_k, _) = _decode_device(dec, syn, rd)
+        assert "cmp_kernel" in bp_k and "ssf_wave_kernel" in ssf_k
+        for key in got:
+            assert np.array_equal(got[key], ref[key]), (extra, key)
+        part, _ = _decode_device(dec, syn, rd, keys=("fail",))
+        assert np.array_equal(part["fail"], ref["fail"])
+        part, _ = _decode_device(dec, syn, rd, keys=("iters", "status"))
+        assert np.array_equal(part["iters"], ref["iters"]) and np.array_equal(part["status"], ref["status"])
+    nofail, _ = _decode_device(dec, syn, None)
+    assert not nofail["fail"].any()
+    assert np.array_equal(nofail["iters"], ref["iters"]) and np.array_equal(nofail["status"], ref["status"])
+
+
+def test_compact_large_batch_counter_tail(gpu_available, oracle_lib, code225):
+    """2^18 shots at p = 0.05 (a compact list long enough for the chunk counter's
+    dynamic tail): a random subset of 3000 shots equals the oracle."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    hz, hx, lz = code225.checks.z, code225.checks.x, code225.logicals.z
+    B, p = 1 << 18, 0.05
+    dec = Decoder(hz, 2 * p / 3, method="ms", precision="f64", max_iter=50, flip_sets=hx, logicals=lz)
+    dev = torch.device("cuda", 0)
+    syn = torch.empty((B, hz.shape[0]), dtype=torch.uint8, device=dev)
+    rd = torch.empty((B, hz.shape[1]), dtype=torch.uint8, device=dev)
+    dec.sample_storage_device(0, p, p, 3, 0, 0, B, syn, rd)
+    out = {k: torch.empty(B, dtype=getattr(torch, dt), device=dev) for k, dt in OUTS}
+    dec.decode_device(B, syn=syn, readout=rd, **out)
+    torch.cuda.synchronize()
+    idx = np.sort(np.random.default_rng(1).choice(B, 3000, replace=False))
+    rs, rr = syn.cpu().numpy()[idx], rd.cpu().numpy()[idx]
+    ref = oracle_lib.decode(hz, 2 * p / 3, rs, method="ms", precision="f64", max_iter=50, ssf=True, gens=hx, lz=lz,
+                            readout=rr, want_llr=False, ssf_impl="fast")
+    for k, v in out.items():
+        assert np.array_equal(v.cpu().numpy()[idx], ref[k]), k

@@ -422,8 +422,20 @@ def test_lds_kernel_ssf_fold(gpu_available, oracle_lib, code225, monkeypatch):
         assert np.array_equal(got[key], ref[key]), key
 
 
+@pytest.fixture(params=["compact", "onepass"])
+def lean_path(request, monkeypatch):
+    """Lean launches run the two-pass compact path (ms_triage_kernel +
+    bp_ms_cmp_kernel) by default; QDEC_COMPACT=0 keeps the one-pass
+    bp_ms_wave_kernel.  Lean tests run both."""
+    if request.param == "onepass":
+        monkeypatch.setenv("QDEC_COMPACT", "0")
+    else:
+        monkeypatch.delenv("QDEC_COMPACT", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("precision,occupancy", [("f64", 0), ("f64", 12), ("f32", 0)])
-def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occupancy):
+def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occupancy, lean_path):
     """The benchmarked instantiation (bp_ms_wave_kernel<.., LEAN=true, ..>, chosen
     when x / corr / llr are all null) pinned bit-exactly: exactly bench.py's
     decode_device call (syn + readout in; iters, status, ssf_steps, fail out) at
@@ -449,6 +461,8 @@ def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occ
                (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
         dec.decode_device(B, syn=syn, readout=rd, **out)
         torch.cuda.synchronize()
+        bp_k, _, pre_k = dec.last_kernels()
+        assert ("cmp_kernel" in bp_k and "triage" in pre_k) == (lean_path == "compact"), (bp_k, pre_k)
         rs, rr = oracle_lib.sample_storage(hz, 0, p, p, seed=seed, stream=pi, shot0=shot0, B=B)
         assert np.array_equal(syn.cpu().numpy(), rs) and np.array_equal(rd.cpu().numpy(), rr), p
         ref = oracle_lib.decode(hz, 2 * p / 3, rs, method="ms", precision=precision, max_iter=50, ssf=True, gens=hx,
@@ -458,7 +472,7 @@ def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occ
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_lean_zero_syndrome_shortcut_and_nonpositive_priors(gpu_available, oracle_lib, precision):
+def test_lean_zero_syndrome_shortcut_and_nonpositive_priors(gpu_available, oracle_lib, precision, lean_path):
     """The LEAN kernel writes iteration 1 / converged / x = 0 directly for an
     all-zero syndrome only when every prior LLR is > 0.  Per-column priors with
     some p >= 0.5 (LLR <= 0: BP must run and need not converge at once) and the
@@ -488,7 +502,7 @@ def test_lean_zero_syndrome_shortcut_and_nonpositive_priors(gpu_available, oracl
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_wave_occupancy_does_not_change_results(gpu_available, oracle_lib, precision):
+def test_wave_occupancy_does_not_change_results(gpu_available, oracle_lib, precision, lean_path):
     """qd_graph_set_wave_occupancy (bench.py's overlapped phases use 12 f64
     waves per CU) only changes the persistent grid: iterations, status, SSF
     steps and failure flags equal the oracle's at 4, 12 and the default; an
@@ -520,7 +534,7 @@ def test_wave_occupancy_does_not_change_results(gpu_available, oracle_lib, preci
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_lean_zero_messages(gpu_available, oracle_lib, precision):
+def test_lean_zero_messages(gpu_available, oracle_lib, precision, lean_path):
     """Exact zero messages on the LEAN kernel.  The f64 LEAN kernel reads ldpc's
     sign test `v <= 0` from sign bits (QDEC_MS_SIGNBIT) and takes a rare path for
     check rows holding a zero entry (+0 or -0).  Priors of exactly 0 (p = 0.5:
