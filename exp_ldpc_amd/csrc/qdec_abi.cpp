@@ -695,7 +695,8 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
         const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
         const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
         const size_t cl = g.wave ? cmp_entry_bytes(g) : 0;
-        const size_t bytes = 256 + (size_t)a.B * (8 + xr) + 256 + (size_t)a.B * cl + 256;
+        const size_t cmp_bytes = g.wave ? (size_t)kCmpSegs * 128 + (size_t)kCmpSegs * cmp_seg_cap(a.B) * cl : 0;
+        const size_t bytes = 256 + ((size_t)a.B * (8 + xr) + 255) / 256 * 256 + 256 + cmp_bytes + 256;
         hip_check(hipMalloc(&G->qws, bytes), "hipMalloc queue");
         G->q_cap = a.B;
     }
@@ -708,8 +709,13 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
     if (g.wave) {
         const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
         const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
-        a.cmp = reinterpret_cast<uint64_t*>(base + 256 + (size_t)G->q_cap * (8 + xr) + 256);
-        a.cmp_count = a.wave_ctr ? a.wave_ctr + 2 : nullptr;
+        // kCmpSegs counters (one 128-B line each: the triage's u64 atomics need
+        // natural alignment, so the region starts on a 256-B boundary), then
+        // the segments
+        uint8_t* cbase = base + 256 + ((size_t)G->q_cap * (8 + xr) + 255) / 256 * 256 + 256;
+        a.cmp_count = reinterpret_cast<unsigned long long*>(cbase);
+        a.cmp = reinterpret_cast<uint64_t*>(cbase + (size_t)kCmpSegs * 128);
+        a.cmp_cap = cmp_seg_cap(G->q_cap);
     }
 }
 

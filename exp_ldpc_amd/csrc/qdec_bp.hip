@@ -35,6 +35,7 @@
 // (popcount of xor with a per-subset mask: 5 VALU ops per subset).  A wave max
 // picks the flip.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 
 #include "qdec_device.h"
@@ -750,6 +751,11 @@ static bool lean_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
 // min-sum launches whose graph has the slot-order logicals (or no fused check);
 // QDEC_COMPACT=0 keeps the one-pass kernel (A/B, parity tests run both).
 static bool compact_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
+    // the triage reads 16-B chunks: 16-B aligned syndrome / readout buffers only;
+    // its list counters take u64 atomics (natural alignment), entries 16-B stores
+    if ((reinterpret_cast<uintptr_t>(a.syn) & 15) || (a.readout && (reinterpret_cast<uintptr_t>(a.readout) & 15)))
+        return false;
+    if ((reinterpret_cast<uintptr_t>(a.cmp_count) & 127) || (reinterpret_cast<uintptr_t>(a.cmp) & 15)) return false;
     const char* v = std::getenv("QDEC_COMPACT");  // read per launch: tests switch it within a process
     const bool off = v && v[0] == '0';
     const bool want_fail = a.fail && a.readout && g.k > 0;
@@ -758,7 +764,17 @@ static bool compact_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
 
 template <int RC, int RV>
 static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t stream) {
-    const size_t lds = 4 * (size_t)(((int64_t)64 * g.m + 3) / 4 + 2 + ((int64_t)64 * g.n_data + 3) / 4 + 2);
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    // the tile loads are 16-B vector loads
+    if ((reinterpret_cast<uintptr_t>(a.syn) & 15) || (want_fail && (reinterpret_cast<uintptr_t>(a.readout) & 15)))
+        return (int)hipErrorInvalidValue;
+    const size_t lds = ((want_fail ? (size_t)g.k * g.lz_words * 8 : 0) + 15) / 16 * 16 +
+                       16 * (size_t)(((int64_t)64 * g.m + 15) / 16 + 2 + ((int64_t)64 * g.n_data + 15) / 16 + 2);
+    if (lds > 64 * 1024) {  // large logical tables (k <= 256, lz_words <= 9)
+        const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ms_triage_kernel<RC, RV>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return (int)ea;
+    }
     QDEC_NOTE_PRE("qdec::ms_triage_kernel", RC, RV);
     hipLaunchKernelGGL((ms_triage_kernel<RC, RV>), dim3((unsigned)((a.B + 63) / 64)), dim3(64), lds, stream, g, a);
     return (int)hipGetLastError();
@@ -783,11 +799,17 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         if (a.q_rpar || (!DEFER && compact_launch(g, a, DEFER))) {  // two passes: triage, then the listed shots
             DecodeArgs b = a;
             b.cmp_zero_ok = (g.ms_allpos >> (sizeof(T) == 4 ? 1 : 0)) & 1;
-            hipError_t e = hipMemsetAsync(b.cmp_count, 0, sizeof(unsigned long long), stream);
+            hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpSegs * 128, stream);
             if (e != hipSuccess) return (int)e;
             int rc = launch_triage<RC, RV>(g, b, stream);
             if (rc != 0) return rc;
-            const size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16;
+            size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16 + 2 * 64 * 8;
+            // a capped grid (f64: 8 waves per CU) must also be placed evenly: the
+            // dispatcher stacks up to the kernel's own occupancy on a CU (11 for
+            // the 159-VGPR f64 kernel) while others sit idle, so the LDS request is
+            // padded to 1/cap of the CU (QDEC_CMP_LDS_PAD=0: unpadded, A/B)
+            const char* pad_env = std::getenv("QDEC_CMP_LDS_PAD");
+            if (cap > 0 && !(pad_env && pad_env[0] == '0')) clds = std::max(clds, (size_t)(160 * 1024 / cap) / 16 * 16);
             // degree-3 rounds: the (2, 4, 7) shape instantiates D3R = 2 (n = 225 HGP: 144 degree-3 columns)
             if constexpr (RC == 2 && RV == 4 && DRC == 7) {
                 if (g.ms_d3r >= 2) {

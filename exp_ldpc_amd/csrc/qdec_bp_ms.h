@@ -750,42 +750,56 @@ struct CmpEntry {
 // bits 24..27 of (d & 0x01010101) * 0x01020408 are bit 0 of d's four bytes
 __device__ __forceinline__ uint32_t byte_bits4(uint32_t d) { return ((d & 0x01010101u) * 0x01020408u) >> 24; }
 
-// Copy bytes [start, start + len) of a buffer of `total` bytes into LDS as the
-// dwords covering them (dst[0] = the dword at or below `start`); returns the
-// byte offset of `start` inside dst.  Coalesced: 64 lanes x 8 dwords per round,
-// all loads of a round issued before any LDS store.  Dwords past the buffer's
-// last whole dword are assembled from byte loads.
-__device__ __forceinline__ int tile_to_lds(const uint8_t* buf, int64_t total, int64_t start, int64_t len,
-                                           uint32_t* dst, int lane) {
-    const int64_t d0 = start >> 2;
-    const int nd = (int)(((start + len + 3) >> 2) - d0);
-    const int64_t whole = total >> 2;  // dwords fully inside the buffer
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(buf) + d0;
-    constexpr int U = 8;
-    for (int b = 0; b < nd; b += 64 * U) {
-        uint32_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int d = b + u * 64 + lane;
-            v[u] = (d < nd && d0 + d < whole) ? __builtin_nontemporal_load(src + d) : 0u;
+// One tile of a shot-major byte buffer, as the 16-B chunks covering bytes
+// [start, start + len) of a buffer of `total` bytes (image chunk 0 = the chunk
+// at or below `start`; `shift` = the byte offset of `start` inside the image).
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+struct TileSrc {
+    const uint8_t* buf;
+    int64_t total, c0;  // c0: first 16-B chunk
+    int nch, shift;
+    u32x4* img;
+    __device__ TileSrc(const uint8_t* b, int64_t tot, int64_t start, int64_t len, u32x4* dst) : buf(b), total(tot), img(dst) {
+        c0 = start >> 4;
+        nch = (int)(((start + len + 15) >> 4) - c0);
+        shift = (int)(start & 15);
+    }
+    // chunk c of the image from its bytes (the buffer's last partial chunk)
+    __device__ u32x4 bytes(int c) const {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int t = 0; t < 16; ++t) {
+            const int64_t q = 16 * (c0 + c) + t;
+            if (q < total) w[t / 4] |= (uint32_t)buf[q] << (8 * (t % 4));
         }
+        return u32x4{w[0], w[1], w[2], w[3]};
+    }
+};
+
+// Copy a tile into its LDS image: U 16-B loads per lane per round (64 U
+// chunks), all issued before any LDS store.  Every load is unconditional, from
+// a chunk index clamped into the buffer's whole 16-B chunks (no exec-masked
+// loads, so the compiler keeps them all in flight); chunks past the buffer's
+// last whole 16 B are assembled from byte loads.  The buffer must be 16-B
+// aligned (the launcher checks; torch allocations are).
+template <int U>
+__device__ __forceinline__ void tile_to_lds(const TileSrc& T, int lane) {
+    const int64_t whole = T.total >> 4;
+    const u32x4* src = reinterpret_cast<const u32x4*>(T.buf);
+    for (int r0 = 0; r0 < T.nch; r0 += 64 * U) {
+        u32x4 v[U];
+        if (whole > 0) {  // uniform
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int d = b + u * 64 + lane;
-            if (d < nd) {
-                uint32_t w = v[u];
-                if (d0 + d >= whole) {  // the buffer's last 1-3 bytes
-                    w = 0u;
-                    for (int t = 0; t < 4; ++t) {
-                        const int64_t q = 4 * (d0 + d) + t;
-                        if (q < total) w |= (uint32_t)buf[q] << (8 * t);
-                    }
-                }
-                dst[d] = w;
+            for (int u = 0; u < U; ++u) {
+                const int64_t gi = min(T.c0 + r0 + u * 64 + lane, whole - 1);
+                v[u] = __builtin_nontemporal_load(src + gi);
             }
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = r0 + u * 64 + lane;
+            if (c < T.nch) T.img[c] = T.c0 + c < whole ? v[u] : T.bytes(c);
+        }
     }
-    return (int)(start & 3);
 }
 
 // NB bytes of a lane's row at byte offset `off` of an LDS dword image, as bit
@@ -819,25 +833,34 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     const int64_t s0 = (int64_t)blockIdx.x * 64;
     const int ns = (int)min((int64_t)64, a.B - s0);
     const bool want_fail = a.fail && a.readout && g.k > 0;
-    uint32_t* syn_img = reinterpret_cast<uint32_t*>(smem);
-    const int syn_dw = (64 * m + 3) / 4 + 2;
-    uint32_t* rd_img = syn_img + syn_dw;
-    const int ssh = tile_to_lds(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img, lane);
-    const int rsh = want_fail ? tile_to_lds(a.readout, a.B * (int64_t)nd, s0 * nd, (int64_t)ns * nd, rd_img, lane) : 0;
+    // LDS: the logicals (k x lz_words u64, read as broadcasts), then the
+    // syndrome and readout tiles as 16-B chunk images (one spare chunk each:
+    // row_bits reads one dword past a row)
+    uint64_t* lz_lds = reinterpret_cast<uint64_t*>(smem);
+    const int nlz = want_fail ? g.k * g.lz_words : 0;
+    u32x4* syn_img = reinterpret_cast<u32x4*>(smem + ((size_t)nlz * 8 + 15) / 16 * 16);
+    u32x4* rd_img = syn_img + (64 * m + 15) / 16 + 2;
+    for (int e = lane; e < nlz; e += 64) lz_lds[e] = g.lz[e];
+    const TileSrc ts(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img);
+    const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
+                     want_fail ? (int64_t)ns * nd : 0, rd_img);
+    tile_to_lds<8>(ts, lane);
+    if (want_fail) tile_to_lds<8>(tr, lane);
     __syncthreads();
+    const int ssh = ts.shift, rsh = tr.shift;
     const bool live = lane < ns;
     const int64_t shot = s0 + lane;
     uint64_t sw[RC];
-    row_bits<RC>(syn_img, ssh + lane * m, m, sw);
+    row_bits<RC>(reinterpret_cast<const uint32_t*>(syn_img), ssh + lane * m, m, sw);
     uint64_t rp[kMaxLogicalRounds] = {0ull, 0ull, 0ull, 0ull};
     if (want_fail) {
         uint64_t rw[NWD];
-        row_bits<NWD>(rd_img, rsh + lane * nd, nd, rw);
-        for (int r = 0; r < g.k; ++r) {  // uniform rows of the dense logical table
+        row_bits<NWD>(reinterpret_cast<const uint32_t*>(rd_img), rsh + lane * nd, nd, rw);
+        for (int r = 0; r < g.k; ++r) {  // uniform rows of the dense logical table (LDS broadcasts)
             int par = 0;
 #pragma unroll
             for (int w = 0; w < NWD; ++w)
-                if (w < g.lz_words) par += __popcll(g.lz[(size_t)r * g.lz_words + w] & rw[w]);
+                if (w < g.lz_words) par += __popcll(lz_word(lz_lds, (size_t)r * g.lz_words + w) & rw[w]);
 #pragma unroll
             for (int rr = 0; rr < kMaxLogicalRounds; ++rr)
                 if (rr == (r >> 6)) rp[rr] |= (uint64_t)(par & 1) << (r & 63);
@@ -856,18 +879,29 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     const bool listed = live && !trivial;
     const unsigned long long bal = __ballot(listed);
     if (bal == 0ull) return;
+    // segment blockIdx % kCmpSegs: 64 counters on their own lines, so the
+    // per-tile atomics do not serialise on one address
+    const int seg = (int)(blockIdx.x % kCmpSegs);
     unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(a.cmp_count, (unsigned long long)__popcll(bal));
+    if (lane == 0) base = atomicAdd(a.cmp_count + 16 * seg, (unsigned long long)__popcll(bal));
     base = __shfl(base, 0);
     if (listed) {
         const uint64_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        uint64_t* e = a.cmp + (base + rank) * Ent::EW;
+        uint64_t* e = a.cmp + ((uint64_t)seg * a.cmp_cap + base + rank) * Ent::EW;
         e[0] = (uint64_t)shot;
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) e[1 + rc] = sw[rc];
 #pragma unroll
         for (int rr = 0; rr < kMaxLogicalRounds; ++rr) e[1 + RC + rr] = rp[rr];
     }
+}
+
+// lane l's copy of v from lane l - off (lanes below off: their own value)
+__device__ __forceinline__ uint64_t readlane64_up(uint64_t v, int off, int lane) {
+    const int src = lane >= off ? lane - off : lane;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // v_readlane of a 64-bit value (lane uniform)
@@ -894,6 +928,15 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
 
     const int lane = threadIdx.x;
     const int m = g.m;
+#ifndef QDEC_CMP_PIN2
+#define QDEC_CMP_PIN2 1
+#endif
+    if constexpr (QDEC_CMP_PIN2 && sizeof(T) == 8 && OCC == 0) {
+        // f64 at 2 waves per SIMD (the one-pass kernel's placement): the kernel
+        // needs ~160 VGPRs, which would let a CU put 3 waves on one SIMD and 1 on
+        // another; claiming v175 makes the allocation 176, so at most 2 per SIMD
+        asm volatile("" ::: "v175");
+    }
     Core core;
     core.load(g, lane);
     Core::init_lds(g, v2c, st, xh, lane);
@@ -902,22 +945,52 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         for (int e = lane; e < g.k * RV; e += 64) lzs[e] = g.ms_lzs[e];
     wave_lds_sync();
 
-    const int64_t count = (int64_t)*a.cmp_count;
-    const int64_t nch = (count + KP - 1) / KP;
+    // chunks of KP entries inside the segments: lane s < kCmpSegs holds segment
+    // s's entry count; cend = inclusive prefix of the segments' chunk counts
+    static_assert(kCmpSegs == 64, "one lane per segment");
+    const int64_t scount = (int64_t)__builtin_nontemporal_load(a.cmp_count + 16 * lane);
+    int64_t cend = (scount + KP - 1) / KP;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t o = (int64_t)readlane64_up((uint64_t)cend, off, lane);
+        cend += lane >= off ? o : 0;
+    }
+    const int64_t nch = (int64_t)readlane64((uint64_t)cend, 63);
+    // kept in LDS (read once per chunk), not in registers across the BP loop
+    int64_t* seg_end = reinterpret_cast<int64_t*>(lzs + (size_t)g.k * RV);  // [64] chunk prefix
+    int64_t* seg_cnt = seg_end + 64;                                       // [64] entries
+    seg_end[lane] = cend;
+    seg_cnt[lane] = scount;
+    wave_lds_sync();
     // the chunk counter only pays when the tail is long (>= 16 chunks per wave)
     unsigned long long* ctr = a.wave_ctr && nch >= 16 * (int64_t)gridDim.x ? a.wave_ctr : nullptr;
     ShotSeq seq(nch, ctr, blockIdx.x, gridDim.x, lane, 1);
+    int ne_n = 0;  // entries in the chunk load_chunk loaded last
     auto load_chunk = [&](int64_t c) -> uint64_t {
-        const int64_t e = c * (KP * EW) + lane;
-        return (c < nch && lane < KP * EW && e < count * EW) ? __builtin_nontemporal_load(a.cmp + e) : 0ull;
+        ne_n = 0;
+        if (c >= nch) return 0ull;
+        const int s = __popcll(__ballot(seg_end[lane] <= c));  // the segment holding chunk c
+        const int64_t c_in = c - (s ? seg_end[s - 1] : 0);
+        const int64_t cnt = seg_cnt[s];
+        ne_n = (int)min((int64_t)KP, cnt - c_in * KP);
+        const int64_t e = ((int64_t)s * a.cmp_cap + c_in * KP) * EW + lane;
+        return lane < ne_n * EW ? __builtin_nontemporal_load(a.cmp + e) : 0ull;
     };
+    // one flat loop over this wave's entries (chunk c, entry q of it; the next
+    // chunk cn is in flight in entn)
+    QDEC_STAMP_DECL
+#ifdef QDEC_STAMPS
+    const unsigned long long qdec_t0 = __builtin_amdgcn_s_memtime();
+#endif
     int64_t c = seq.next(lane);
     uint64_t ent = load_chunk(c);
+    int ne = ne_n;
+    int64_t cn = c < nch ? seq.next(lane) : nch;
+    uint64_t entn = load_chunk(cn);
+    int q = 0;
+    QDEC_STAMP(4);  // prologue
     while (c < nch) {
-        const int64_t cn = seq.next(lane);
-        const uint64_t entn = load_chunk(cn);
-        const int ne = (int)min((int64_t)KP, count - c * KP);
-        for (int q = 0; q < ne; ++q) {
+        {
             const int64_t shot = (int64_t)readlane64(ent, q * EW);
             bool sbit[RC];
 #pragma unroll
@@ -927,12 +1000,16 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
             for (int rr = 0; rr < kMaxLogicalRounds; ++rr) rpar[rr] = readlane64(ent, q * EW + 1 + RC + rr);
             core.write_priors(v2c);
             wave_lds_sync();
+            QDEC_STAMP(0);  // entry + initial messages
             T Q[RV];
             uint64_t X[RV];
             bool pres[RC];
             int it = 1;
             const bool conv = core.iterate(a, v2c, st, m, lane, sbit, Q, X, pres, it);
             const int iters = conv ? it : a.max_iter;
+            QDEC_STAMP(1);  // BP iterations
+            QDEC_COUNT(8, iters);
+            QDEC_COUNT(9, 1);
             if (lane == 0 && a.iters) a.iters[shot] = iters;
             if (DEFER && !conv) {
                 // hard decision by column for the SSF queue (slot order -> xh[column])
@@ -971,9 +1048,22 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
                 }
             }
         }
-        c = cn;
-        ent = entn;
+        QDEC_STAMP(2);  // failure check, outputs / SSF queue
+        if (++q == ne) {  // next chunk
+            q = 0;
+            c = cn;
+            ent = entn;
+            ne = ne_n;
+            cn = c < nch ? seq.next(lane) : nch;
+            entn = load_chunk(cn);
+            QDEC_STAMP(3);  // chunk hand-off
+        }
     }
+#ifdef QDEC_STAMPS
+    QDEC_COUNT(10, __builtin_amdgcn_s_memtime() - qdec_t0);
+    QDEC_COUNT(12, 1);
+#endif
+    QDEC_FLUSH_AT(32);
 }
 
 }  // namespace qdec

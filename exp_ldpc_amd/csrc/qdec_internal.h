@@ -17,6 +17,9 @@ constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
 constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
 constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
 constexpr int kEdgePad = 16;     // index / prior arrays padded past E (>= the largest row / column width)
+constexpr int kCmpSegs = 64;     // segments (and counters) of the compact shot list
+// entries a compact-list segment must hold for a batch of B shots (64-shot tiles)
+inline int64_t cmp_seg_cap(int64_t B) { return ((B + 63) / 64 + kCmpSegs - 1) / kCmpSegs * 64; }
 
 // Wave-kernel shapes (check rounds RC, variable rounds RV, check-node compute
 // width D <= kDR): a graph is padded to the first shape that holds it (RC*64 >= m,
@@ -166,10 +169,13 @@ struct DecodeArgs {
     // before the BP kernel, after it, and after the SSF kernel
     hipEvent_t* ev;    // [3] or nullptr
     // compact shot list of lean min-sum wave launches (ms_triage_kernel ->
-    // bp_ms_cmp_kernel): entries [B][CmpEntry::EW] u64, count at cmp_count
-    // (zeroed by the launcher); nullptr -> no compact path
+    // bp_ms_cmp_kernel), in kCmpSegs segments: triage tile t appends to
+    // segment t % kCmpSegs, whose entries [cmp_cap][CmpEntry::EW] u64 start at
+    // cmp + s * cmp_cap * EW, counted at cmp_count[s * 16] (one 128-B line per
+    // counter; zeroed by the launcher).  nullptr -> no compact path
     uint64_t* cmp;
     unsigned long long* cmp_count;
+    int64_t cmp_cap;
     int cmp_zero_ok;  // every prior of the launch's precision > 0: zero syndromes finish in the triage
     // packed SSF queue entries carry the readout's logical parities (bit r of
     // the dw area = parity of Lz[r] . readout) instead of the readout words

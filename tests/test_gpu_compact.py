@@ -128,3 +128,32 @@ def test_compact_large_batch_counter_tail(gpu_available, oracle_lib, code225):
                             readout=rr, want_llr=False, ssf_impl="fast")
     for k, v in out.items():
         assert np.array_equal(v.cpu().numpy()[idx], ref[k]), k
+
+
+def test_misaligned_buffers_take_the_one_pass_kernel(gpu_available, oracle_lib, code225):
+    """The triage reads 16-B chunks, so syndrome / readout views that do not start
+    on a 16-B boundary run the one-pass kernel instead (same results)."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    hz, hx, lz = code225.checks.z, code225.checks.x, code225.logicals.z
+    rng = np.random.default_rng(9)
+    B, (m, n) = 777, hz.shape
+    e = (rng.random((B, n)) < 0.02).astype(np.uint8)
+    syn = ((hz @ e.T).T % 2).astype(np.uint8)
+    rd = (e ^ (rng.random((B, n)) < 0.002)).astype(np.uint8)
+    dev = torch.device("cuda", 0)
+    sbuf = torch.zeros(B * m + 16, dtype=torch.uint8, device=dev)
+    rbuf = torch.zeros(B * n + 16, dtype=torch.uint8, device=dev)
+    sv = sbuf[3:3 + B * m].view(B, m)
+    rv = rbuf[5:5 + B * n].view(B, n)
+    sv.copy_(torch.from_numpy(syn))
+    rv.copy_(torch.from_numpy(rd))
+    dec = Decoder(hz, 0.013, method="ms", precision="f64", max_iter=50, flip_sets=hx, logicals=lz)
+    out = {k: torch.empty(B, dtype=getattr(torch, dt), device=dev) for k, dt in OUTS}
+    dec.decode_device(B, syn=sv, readout=rv, **out)
+    torch.cuda.synchronize()
+    assert "bp_ms_wave_kernel" in dec.last_kernels()[0]
+    ref = oracle_lib.decode(hz, 0.013, syn, method="ms", precision="f64", max_iter=50, ssf=True, gens=hx, lz=lz,
+                            readout=rd, want_llr=False, ssf_impl="fast")
+    for k, v in out.items():
+        assert np.array_equal(v.cpu().numpy(), ref[k]), k
