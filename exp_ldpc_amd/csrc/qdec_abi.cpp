@@ -464,6 +464,80 @@ tables_done:
     g.ms_smask = G->arena.upload(smask);
 }
 
+// Iteration 1 of lean min-sum as a table per column, for ms_triage_kernel.
+// With every prior L > 0 nothing in the first check pass depends on signs but
+// the syndrome: check i sends column j the message (s_i ? -1 : 1) * alpha_1 *
+// (L_j == m1_i ? m2_i : m1_i), m1 / m2 the two smallest priors on row i (Big
+// where the row has fewer: the kernels' unused row positions), alpha_1 = 1 -
+// 2^-1 = 0.5 (exact).  So column j's decision after iteration 1 (posterior
+// L_j + sum of the messages <= 0) is a function of its <= 4 checks' syndrome
+// bits.  It is evaluated here in the kernels' precision and summation order
+// (MsCore::iterate: edges by ascending row, acc += c_k), so the table is the
+// kernel's decision bit for bit; bit b = the decision under pattern b (bit k =
+// the syndrome bit of edge k's check).
+template <typename T>
+static std::vector<uint16_t> it1_lut(const qd_graph* G, const std::vector<T>& L, T big) {
+    const DevGraph& g = G->dg;
+    std::vector<T> m1(g.m, big), m2(g.m, big);
+    for (int i = 0; i < g.m; ++i)
+        for (int e = G->row_ptr[i]; e < G->row_ptr[i + 1]; ++e) {
+            const T av = std::fabs(L[G->col_idx[e]]);  // the med3 chain / top-2 tree of the check pass
+            if (av < m1[i]) {
+                m2[i] = m1[i];
+                m1[i] = av;
+            } else if (av < m2[i]) {
+                m2[i] = av;
+            }
+        }
+    std::vector<uint16_t> lut(g.n_pad, 0);
+    for (int j = 0; j < g.n; ++j) {
+        const int t0 = G->col_ptr[j], deg = G->col_ptr[j + 1] - t0;
+        T y[kDC];
+        for (int k = 0; k < deg; ++k) {
+            const int i = G->col_rows[t0 + k];
+            y[k] = (L[j] == m1[i] ? m2[i] : m1[i]) * (T)0.5;
+        }
+        uint32_t bits = 0;
+        for (int b = 0; b < (1 << deg); ++b) {
+            T acc = L[j];
+            for (int k = 0; k < deg; ++k) acc = acc + (((b >> k) & 1) ? -y[k] : y[k]);
+            if (acc <= (T)0) bits |= 1u << b;
+        }
+        lut[j] = (uint16_t)bits;
+    }
+    return lut;
+}
+
+// The precision-independent part: checks of each column, columns of each row.
+static void it1_tables(qd_graph* G, bool pos64, const std::vector<double>& L64, bool pos32,
+                       const std::vector<float>& L32) {
+    DevGraph& g = G->dg;
+    g.it1_vchk = nullptr;
+    g.it1_cvar = nullptr;
+    g.it1_lut[QD_F64] = g.it1_lut[QD_F32] = nullptr;
+    if (!g.wave || g.max_cdeg > kDC || g.max_rdeg > kDR || g.m > 0xfffe || g.n > 0xfffe) return;
+    std::vector<uint64_t> vchk(g.n_pad, 0), cvar(2 * (size_t)g.m_pad, 0);
+    for (int j = 0; j < g.n_pad; ++j) {
+        uint64_t w = 0;
+        for (int k = 0; k < kDC; ++k) {
+            const int t = j < g.n ? G->col_ptr[j] + k : 0;
+            const int i = (j < g.n && t < G->col_ptr[j + 1]) ? G->col_rows[t] : g.m;
+            w |= (uint64_t)i << (16 * k);
+        }
+        vchk[j] = w;
+    }
+    for (int i = 0; i < g.m_pad; ++i)
+        for (int t = 0; t < kDR; ++t) {
+            const int e = i < g.m ? G->row_ptr[i] + t : 0;
+            const int j = (i < g.m && e < G->row_ptr[i + 1]) ? G->col_idx[e] : g.n;
+            cvar[2 * (size_t)i + t / 4] |= (uint64_t)j << (16 * (t % 4));
+        }
+    g.it1_vchk = G->prior_arena.upload(vchk);
+    g.it1_cvar = G->prior_arena.upload(cvar);
+    if (pos64) g.it1_lut[QD_F64] = G->prior_arena.upload(it1_lut<double>(G, L64, 1e308));
+    if (pos32) g.it1_lut[QD_F32] = G->prior_arena.upload(it1_lut<float>(G, L32, 1e30f));
+}
+
 // Row positions of the edges for the LDS-resident min-sum kernel
 // (bp_ms_lds_kernel): edge e of row i sits at LDS element i * kMlDRS + pos[e].
 // The check pass is independent of the order inside a row, so positions are
@@ -1193,6 +1267,7 @@ int qd_graph_set_priors(qd_graph* G, const double* probs) {
                 pos32 = pos32 && ms32[j] > 0.0f;
             }
             g.ms_allpos = (pos64 ? 1 << QD_F64 : 0) | (pos32 ? 1 << QD_F32 : 0);
+            it1_tables(G, pos64, ms64, pos32, ms32);
         }
         g.prior[QD_PRODUCT_SUM][QD_F64] = G->prior_arena.upload(ps64);
         g.prior[QD_PRODUCT_SUM][QD_F32] = G->prior_arena.upload(ps32);

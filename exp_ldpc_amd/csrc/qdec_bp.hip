@@ -768,8 +768,12 @@ static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t str
     // the tile loads are 16-B vector loads
     if ((reinterpret_cast<uintptr_t>(a.syn) & 15) || (want_fail && (reinterpret_cast<uintptr_t>(a.readout) & 15)))
         return (int)hipErrorInvalidValue;
+    if (a.it1_lut && (!g.it1_vchk || !g.it1_cvar || g.m_pad != 64 * RC || g.n_pad != 64 * RV))
+        return (int)hipErrorInvalidValue;
+    // the logicals, then the tile images, which the iteration-1 words reuse
+    const size_t tiles = 16 * (size_t)(((int64_t)64 * g.m + 15) / 16 + 2 + ((int64_t)64 * g.n_data + 15) / 16 + 2);
     const size_t lds = ((want_fail ? (size_t)g.k * g.lz_words * 8 : 0) + 15) / 16 * 16 +
-                       16 * (size_t)(((int64_t)64 * g.m + 15) / 16 + 2 + ((int64_t)64 * g.n_data + 15) / 16 + 2);
+                       std::max(tiles, a.it1_lut ? TriageIt1<RC, RV>::bytes : (size_t)0);
     if (lds > 64 * 1024) {  // large logical tables (k <= 256, lz_words <= 9)
         const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ms_triage_kernel<RC, RV>),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -799,6 +803,12 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         if (a.q_rpar || (!DEFER && compact_launch(g, a, DEFER))) {  // two passes: triage, then the listed shots
             DecodeArgs b = a;
             b.cmp_zero_ok = (g.ms_allpos >> (sizeof(T) == 4 ? 1 : 0)) & 1;
+            // iteration 1 in the triage: the tables assume alpha_1 = 0.5 (the
+            // default schedule); QDEC_TRIAGE_IT1=0 leaves it to the BP kernel (A/B)
+            const char* it1_env = std::getenv("QDEC_TRIAGE_IT1");
+            b.it1_lut = (a.ms_scaling == 0.0 && a.max_iter >= 1 && !(it1_env && it1_env[0] == '0'))
+                            ? g.it1_lut[sizeof(T) == 4 ? 1 : 0]
+                            : nullptr;
             hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpSegs * 128, stream);
             if (e != hipSuccess) return (int)e;
             int rc = launch_triage<RC, RV>(g, b, stream);

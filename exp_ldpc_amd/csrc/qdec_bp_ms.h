@@ -823,6 +823,62 @@ __device__ __forceinline__ void row_bits(const uint32_t* img, int off, int len, 
     }
 }
 
+// Iteration 1 in the triage (DecodeArgs::it1_lut), bit-sliced over the tile's
+// 64 shots: the syndrome is transposed to one word per check (bit s = shot s),
+// each column's decision word is its 16-bit table (it1_tables, qdec_abi.cpp)
+// applied to its <= 4 checks' words, and a shot whose decision meets its
+// syndrome has converged in iteration 1 -- the BP kernel would report exactly
+// that (iterations 1, status 3, failure = parity of Lz x against the readout).
+// LDS (over the tile images, dead by then): check words [RC*64 + 1] (the last
+// one zero: pad check id), decision words [RV*64 + 1] (the last zero: pad
+// column id), logical parities [256].
+template <int RC, int RV>
+struct TriageIt1 {
+    static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
+};
+
+#ifndef QDEC_T1_BALLOT
+#define QDEC_T1_BALLOT 0  // 1: transpose by 64 ballots per word (A/B)
+#endif
+// 64 x 64 bit transpose across the wave: lane r holds row r (bit c = entry
+// (r, c)), and gets back column r (bit c = entry (c, r)).  Six block-swap
+// stages, each one exchange with lane ^ j: the off-diagonal j x j blocks of
+// every 2j x 2j block trade places.
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t v, int lane) {
+    const uint64_t keep[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const int j = 32 >> st;
+        const uint64_t k0 = keep[st];  // columns c with (c & j) == 0
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, j);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), j);
+        const uint64_t w = ((uint64_t)hi << 32) | lo;
+        v = (lane & j) ? ((v & ~k0) | ((w >> j) & k0)) : ((v & k0) | ((w & k0) << j));
+    }
+    return v;
+}
+
+// f(w0..w3) of a 16-entry truth table, bit-sliced: OR over the patterns p with
+// table bit p of the minterm (w_k or ~w_k by bit k of p)
+__device__ __forceinline__ uint64_t lut4_words(uint32_t lut, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
+    const uint64_t A[4] = {~w0 & ~w1, w0 & ~w1, ~w0 & w1, w0 & w1};
+    const uint64_t C[4] = {~w2 & ~w3, w2 & ~w3, ~w2 & w3, w2 & w3};
+    uint64_t f = 0ull;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint64_t gsel = 0ull;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            // all-ones / zero from table bit q + 4r
+            const int64_t msk = -(int64_t)((lut >> (q + 4 * r)) & 1u);
+            gsel |= A[q] & (uint64_t)msk;
+        }
+        f |= gsel & C[r];
+    }
+    return f;
+}
+
 // One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).
 template <int RC, int NWD>
 __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
@@ -841,6 +897,21 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     u32x4* syn_img = reinterpret_cast<u32x4*>(smem + ((size_t)nlz * 8 + 15) / 16 * 16);
     u32x4* rd_img = syn_img + (64 * m + 15) / 16 + 2;
     for (int e = lane; e < nlz; e += 64) lz_lds[e] = g.lz[e];
+    // iteration-1 tables (TriageIt1), loaded ahead of the tiles
+    uint64_t it_ids[NWD], it_cv[RC][2];
+    uint32_t it_lut[NWD];
+    if (a.it1_lut) {
+#pragma unroll
+        for (int rv = 0; rv < NWD; ++rv) {
+            it_ids[rv] = g.it1_vchk[rv * 64 + lane];
+            it_lut[rv] = a.it1_lut[rv * 64 + lane];
+        }
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) {
+            it_cv[rc][0] = g.it1_cvar[2 * (rc * 64 + lane)];
+            it_cv[rc][1] = g.it1_cvar[2 * (rc * 64 + lane) + 1];
+        }
+    }
     const TileSrc ts(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img);
     const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
                      want_fail ? (int64_t)ns * nd : 0, rd_img);
@@ -866,15 +937,96 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
                 if (rr == (r >> 6)) rp[rr] |= (uint64_t)(par & 1) << (r & 63);
         }
     }
-    uint64_t any = 0ull;
+    bool trivial;
+    uint8_t fbit;
+    // iteration 1 pays only where shots converge in it: tiles with >= 8 shots of
+    // syndrome weight <= 12 (about three isolated errors); others just list
+    int wt = 0;
 #pragma unroll
-    for (int rc = 0; rc < RC; ++rc) any |= sw[rc];
-    const bool trivial = live && any == 0ull && a.cmp_zero_ok;
+    for (int rc = 0; rc < RC; ++rc) wt += __popcll(sw[rc]);
+    const bool it1 = a.it1_lut && __popcll(__ballot(live && wt <= 12)) >= 8;
+    if (it1) {  // uniform: iteration 1 here (TriageIt1)
+        // in the tile images' place (dead once the rows are bit words)
+        wave_lds_sync();
+        uint64_t* synT = reinterpret_cast<uint64_t*>(syn_img);
+        uint64_t* xT = synT + RC * 64 + 1;
+        uint64_t* lzp = xT + NWD * 64 + 1;
+        // transpose: lane t gets the word of check rc * 64 + t
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) {
+#if QDEC_T1_BALLOT
+            uint64_t mine = 0ull;
+#pragma unroll
+            for (int t = 0; t < 64; ++t) {
+                const uint64_t wd = __ballot(live && ((sw[rc] >> t) & 1ull));
+                mine = lane == t ? wd : mine;
+            }
+#else
+            const uint64_t mine = wave_transpose64(live ? sw[rc] : 0ull, lane);
+#endif
+            synT[rc * 64 + lane] = mine;  // checks >= m: zero words
+        }
+        if (lane == 0) {
+            synT[RC * 64] = 0ull;
+            xT[NWD * 64] = 0ull;
+        }
+        wave_lds_sync();
+        // decision words, one column per lane
+#pragma unroll
+        for (int rv = 0; rv < NWD; ++rv) {
+            const uint64_t ids = it_ids[rv];
+            xT[rv * 64 + lane] = lut4_words(it_lut[rv], synT[ids & 0xffff], synT[(ids >> 16) & 0xffff],
+                                            synT[(ids >> 32) & 0xffff], synT[ids >> 48]);
+        }
+        wave_lds_sync();
+        // residual syndrome words, one check per lane, OR-reduced over the wave
+        uint64_t bad = 0ull;
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) {
+            const uint64_t c0 = it_cv[rc][0], c1 = it_cv[rc][1];
+            uint64_t par = synT[rc * 64 + lane];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) par ^= xT[(c0 >> (16 * t)) & 0xffff] ^ xT[(c1 >> (16 * t)) & 0xffff];
+            bad |= par;
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)bad, off);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(bad >> 32), off);
+            bad |= ((uint64_t)hi << 32) | lo;
+        }
+        trivial = live && !((bad >> lane) & 1ull);
+        int f = 0;
+        if (want_fail && __ballot(trivial)) {
+            // parity words of the logicals (one logical per lane: the set bits of
+            // its row of the dense table), then each shot's bits
+            for (int r = lane; r < g.k; r += 64) {
+                uint64_t p = 0ull;
+                for (int w = 0; w < g.lz_words; ++w)
+                    for (uint64_t bits = lz_word(lz_lds, (size_t)r * g.lz_words + w); bits; bits &= bits - 1ull)
+                        p ^= xT[w * 64 + __builtin_ctzll(bits)];
+                lzp[r] = p;
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                const int nr = min(64, g.k - rr * 64);
+                for (int t = 0; t < nr; ++t) f |= (int)(((lzp[rr * 64 + t] >> lane) ^ (rp[rr] >> t)) & 1ull);
+            }
+        }
+        fbit = (uint8_t)f;
+    } else {
+        uint64_t any = 0ull;
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) any |= sw[rc];
+        trivial = live && any == 0ull && a.cmp_zero_ok;
+        fbit = (uint8_t)((rp[0] | rp[1] | rp[2] | rp[3]) != 0ull);
+    }
     if (live && trivial) {
         if (a.iters) a.iters[shot] = 1;
         if (a.status) a.status[shot] = 3;
         if (a.ssf_steps) a.ssf_steps[shot] = 0;
-        if (a.fail) a.fail[shot] = (uint8_t)((rp[0] | rp[1] | rp[2] | rp[3]) != 0ull);
+        if (a.fail) a.fail[shot] = want_fail ? fbit : (uint8_t)0;
     }
     const bool listed = live && !trivial;
     const unsigned long long bal = __ballot(listed);
@@ -912,8 +1064,9 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 }
 
 // The compact-list BP kernel (see above): the lean bp_ms_wave_kernel's BP
-// (MsCore) on the listed shots only.  Entries come in chunks of CmpEntry::kPer
-// (one u64 per lane, the next chunk loaded while this one decodes); chunks are
+// (MsCore) on the listed shots only.  Entries come in chunks of up to
+// CmpEntry::kPer (one u64 per lane, the next chunk loaded while this one
+// decodes; a list shorter than kPer entries per wave is cut finer); chunks are
 // handed out by ShotSeq (static stride, then a counter for the tail).
 template <typename T, int RC, int RV, int DRC, bool DEFER, int D3R, int OCC = 0>
 __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void bp_ms_cmp_kernel(DevGraph g, DecodeArgs a) {
@@ -949,7 +1102,17 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     // s's entry count; cend = inclusive prefix of the segments' chunk counts
     static_assert(kCmpSegs == 64, "one lane per segment");
     const int64_t scount = (int64_t)__builtin_nontemporal_load(a.cmp_count + 16 * lane);
-    int64_t cend = (scount + KP - 1) / KP;
+    // entries per chunk: KP, fewer when the list is short (below KP entries per
+    // wave the decode is latency-bound: spread the shots over more waves)
+    int64_t tot = scount;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t o = (int64_t)readlane64_up((uint64_t)tot, off, lane);
+        tot += lane >= off ? o : 0;
+    }
+    tot = (int64_t)readlane64((uint64_t)tot, 63);
+    const int kp = (int)min((int64_t)KP, max((int64_t)1, (tot + gridDim.x - 1) / gridDim.x));
+    int64_t cend = (scount + kp - 1) / kp;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const int64_t o = (int64_t)readlane64_up((uint64_t)cend, off, lane);
@@ -972,8 +1135,8 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         const int s = __popcll(__ballot(seg_end[lane] <= c));  // the segment holding chunk c
         const int64_t c_in = c - (s ? seg_end[s - 1] : 0);
         const int64_t cnt = seg_cnt[s];
-        ne_n = (int)min((int64_t)KP, cnt - c_in * KP);
-        const int64_t e = ((int64_t)s * a.cmp_cap + c_in * KP) * EW + lane;
+        ne_n = (int)min((int64_t)kp, cnt - c_in * kp);
+        const int64_t e = ((int64_t)s * a.cmp_cap + c_in * kp) * EW + lane;
         return lane < ne_n * EW ? __builtin_nontemporal_load(a.cmp + e) : 0ull;
     };
     // one flat loop over this wave's entries (chunk c, entry q of it; the next

@@ -89,6 +89,15 @@ struct DevGraph {
     const void* ms_prior[2];      // [precision][n_pad] min-sum priors in slot order
     int ms_d3r;                   // leading 64-slot rounds whose variables all have degree <= 3
     int ms_allpos;                // bit p: every prior LLR of precision p is > 0
+    // iteration 1 of min-sum inside the triage (ms_triage_kernel, qdec_bp_ms.h):
+    // the checks of column j's edges in edge order (4 x u16, pad -> m), the
+    // columns of check i's row (8 x u16 over two words, pad -> n), and per
+    // precision each column's hard decision after iteration 1 as a 16-bit table
+    // over its checks' syndrome bits (nullptr unless every prior of that
+    // precision is > 0; it1_tables in qdec_abi.cpp)
+    const uint64_t* it1_vchk;     // [n_pad]
+    const uint64_t* it1_cvar;     // [m_pad][2]
+    const uint16_t* it1_lut[2];   // [precision][n_pad]
     int wave_occ;                 // qd_graph_set_wave_occupancy (0: default)
     // LDS-resident min-sum workgroup kernel (qdec_bp_block.hip, bp_ms_lds_kernel):
     // [kMlDC][n] LDS element of edge k of column j (row * kMlDRS + CSR position),
@@ -177,6 +186,10 @@ struct DecodeArgs {
     unsigned long long* cmp_count;
     int64_t cmp_cap;
     int cmp_zero_ok;  // every prior of the launch's precision > 0: zero syndromes finish in the triage
+    // the triage runs iteration 1 itself (g.it1_lut of the launch's precision;
+    // set by the launcher when the schedule's alpha_1 is 0.5): shots whose
+    // iteration-1 decision meets the syndrome finish there
+    const uint16_t* it1_lut;
     // packed SSF queue entries carry the readout's logical parities (bit r of
     // the dw area = parity of Lz[r] . readout) instead of the readout words
     int q_rpar;

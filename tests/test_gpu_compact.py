@@ -71,6 +71,51 @@ def test_compact_every_wave_shape(gpu_available, oracle_lib, precision, mn, monk
             assert "bp_ms_wave_kernel" in bp1
             for key in got:
                 assert np.array_equal(one[key], got[key]), (k, B, key)
+            # iteration 1 left to the BP kernel (the triage only lists)
+            monkeypatch.setenv("QDEC_TRIAGE_IT1", "0")
+            lst, _ = _decode_device(dec, syn, rd)
+            monkeypatch.delenv("QDEC_TRIAGE_IT1")
+            for key in got:
+                assert np.array_equal(lst[key], got[key]), (k, B, key)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_triage_iteration_one_edges(gpu_available, oracle_lib, precision):
+    """The triage's iteration-1 tables (it1_tables, qdec_abi.cpp) against the
+    oracle where they are most fragile: priors with exact ties between columns
+    (the m1 == L_j selection), degree-1 rows (m2 = Big), columns of degree 1..4,
+    single-error shots (most converge in iteration 1) next to heavier ones; a
+    non-default scaling (tables off) and a negative prior (tables off) give the
+    oracle's results too."""
+    from exp_ldpc_amd.decoder import Decoder
+    rng = np.random.default_rng(77)
+    m, n = 96, 150
+    H = _random_graph(rng, m, n, dmax=6)
+    light = np.flatnonzero(np.diff(sp.csc_matrix(H).indptr) < 4)[[0, 7, 20]]  # room for one more edge
+    H = sp.vstack([H, sp.csr_matrix((np.ones(3), ([0, 1, 2], light)), shape=(3, n))]).tocsr()
+    levels = np.array([0.01, 0.02, 0.02, 0.04, 0.011])
+    probs = levels[rng.integers(0, len(levels), n)]
+    B = 2500
+    e = np.zeros((B, n), np.uint8)
+    e[np.arange(B), rng.integers(0, n, B)] = 1  # one error per shot
+    e[B // 2:] |= (rng.random((B - B // 2, n)) < 0.02).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    rd = (e ^ (rng.random((B, n)) < 0.005)).astype(np.uint8)
+    L = (rng.random((5, n)) < 0.1).astype(np.uint8)
+    cases = [(probs, 0.0), (probs, 0.625)]
+    neg = probs.copy()
+    neg[7] = 0.7  # a negative prior LLR
+    cases.append((neg, 0.0))
+    for pr, scaling in cases:
+        dec = Decoder(H, pr, method="ms", precision=precision, max_iter=25, ms_scaling=scaling, logicals=L)
+        got, (bp_k, _, pre_k) = _decode_device(dec, syn, rd)
+        assert "cmp_kernel" in bp_k and "triage" in pre_k
+        ref = oracle_lib.decode(H, pr, syn, method="ms", precision=precision, max_iter=25, ms_scaling=scaling, lz=L,
+                                readout=rd, want_llr=False)
+        for key in got:
+            assert np.array_equal(got[key], ref[key]), (scaling, key)
+        if scaling == 0.0 and pr is probs:
+            assert (ref["iters"] == 1).mean() > 0.3  # the triage's share is real
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
