@@ -791,7 +791,8 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         // (lz_in_lds); wave-kernel graphs always have one (n <= 576)
         if (a.fail && g.k > 0 && !g.lz) return (int)hipErrorInvalidValue;
         const size_t lds = MsLds<T>::template bytes<RC, RV>(g);
-        if (a.wave_ctr) {  // ShotSeq's chunk counter
+        const bool two_pass = a.q_rpar || (!DEFER && compact_launch(g, a, DEFER));
+        if (a.wave_ctr && !two_pass) {  // ShotSeq's chunk counter (two passes: the triage zeroes it)
             const hipError_t e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);
             if (e != hipSuccess) return (int)e;
         }
@@ -800,7 +801,7 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
         // p (n = 225: 7.1 vs 9.3 ms per 2^18 shots at p = 0.1); concurrent
         // decodes may ask for more (qd_graph_set_wave_occupancy)
         const int cap = g.wave_occ > 0 ? g.wave_occ : (sizeof(T) == 8 ? 8 : 0);
-        if (a.q_rpar || (!DEFER && compact_launch(g, a, DEFER))) {  // two passes: triage, then the listed shots
+        if (two_pass) {  // triage, then the listed shots
             DecodeArgs b = a;
             b.cmp_zero_ok = (g.ms_allpos >> (sizeof(T) == 4 ? 1 : 0)) & 1;
             // iteration 1 in the triage: the tables assume alpha_1 = 0.5 (the
@@ -892,10 +893,12 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hip
         return rc;
     }
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
-    if (e == hipSuccess && a.wave_ctr)  // the SSF kernel's slot counter (ShotSeq)
-        e = hipMemsetAsync(a.wave_ctr + 1, 0, sizeof(unsigned long long), stream);
-    if (e != hipSuccess) return (int)e;
+    if (!a.q_rpar) {  // the compact path's triage zeroes both counters itself (one launch fewer each)
+        hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
+        if (e == hipSuccess && a.wave_ctr)  // the SSF kernel's slot counter (ShotSeq)
+            e = hipMemsetAsync(a.wave_ctr + 1, 0, sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return (int)e;
+    }
     record_ev(a, 0, stream);
     int rc = launch_bp_wave<T, METHOD, RC, RV, DRC, true>(g, a, num_cus, stream);
     record_ev(a, 1, stream);

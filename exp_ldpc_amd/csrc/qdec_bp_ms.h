@@ -802,6 +802,38 @@ __device__ __forceinline__ void tile_to_lds(const TileSrc& T, int lane) {
     }
 }
 
+// Two tiles (syndrome and readout) into their LDS images with every load of a
+// round issued before any LDS store, so the second tile's HBM latency overlaps
+// the first's: UA / UB 16-B loads per lane per round (the bench shape does
+// both tiles in one round).  Same clamping and tail handling as tile_to_lds.
+template <int UA, int UB>
+__device__ __forceinline__ void tile_pair_to_lds(const TileSrc& A, const TileSrc& B, int lane) {
+    const int64_t wa = A.total >> 4, wb = B.total >> 4;
+    const u32x4* sa = reinterpret_cast<const u32x4*>(A.buf);
+    const u32x4* sb = reinterpret_cast<const u32x4*>(B.buf);
+    for (int ra = 0, rb = 0; ra < A.nch || rb < B.nch; ra += 64 * UA, rb += 64 * UB) {
+        u32x4 va[UA], vb[UB];
+        if (wa > 0 && ra < A.nch) {  // uniform
+#pragma unroll
+            for (int u = 0; u < UA; ++u) va[u] = __builtin_nontemporal_load(sa + min(A.c0 + ra + u * 64 + lane, wa - 1));
+        }
+        if (wb > 0 && rb < B.nch) {  // uniform
+#pragma unroll
+            for (int u = 0; u < UB; ++u) vb[u] = __builtin_nontemporal_load(sb + min(B.c0 + rb + u * 64 + lane, wb - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < UA; ++u) {
+            const int c = ra + u * 64 + lane;
+            if (c < A.nch) A.img[c] = A.c0 + c < wa ? va[u] : A.bytes(c);
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            const int c = rb + u * 64 + lane;
+            if (c < B.nch) B.img[c] = B.c0 + c < wb ? vb[u] : B.bytes(c);
+        }
+    }
+}
+
 // NB bytes of a lane's row at byte offset `off` of an LDS dword image, as bit
 // words (bit i of word i/64 = bit 0 of byte i); bytes >= len are cleared.
 template <int NW>
@@ -837,6 +869,9 @@ struct TriageIt1 {
     static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
 };
 
+#ifndef QDEC_TRIAGE_PAIR
+#define QDEC_TRIAGE_PAIR 1  // 0: the syndrome tile, then the readout tile (A/B)
+#endif
 #ifndef QDEC_T1_BALLOT
 #define QDEC_T1_BALLOT 0  // 1: transpose by 64 ballots per word (A/B)
 #endif
@@ -889,6 +924,14 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     const int64_t s0 = (int64_t)blockIdx.x * 64;
     const int ns = (int)min((int64_t)64, a.B - s0);
     const bool want_fail = a.fail && a.readout && g.k > 0;
+    // the launch's counters that run behind this pass (compact-kernel chunk
+    // counter, SSF slot counter, SSF queue length) are zeroed here, saving a
+    // memset launch each (the previous decode on the handle has finished with
+    // them: the workspace chain orders decodes)
+    if (blockIdx.x == 0 && lane == 0) {
+        if (a.wave_ctr) a.wave_ctr[0] = a.wave_ctr[1] = 0ull;
+        if (a.q_count) *a.q_count = 0;
+    }
     // LDS: the logicals (k x lz_words u64, read as broadcasts), then the
     // syndrome and readout tiles as 16-B chunk images (one spare chunk each:
     // row_bits reads one dword past a row)
@@ -915,8 +958,13 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     const TileSrc ts(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img);
     const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
                      want_fail ? (int64_t)ns * nd : 0, rd_img);
+#if QDEC_TRIAGE_PAIR
+    if (want_fail) tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < 16 ? 4 * NWD : 16)>(ts, tr, lane);
+    else tile_to_lds<8>(ts, lane);
+#else
     tile_to_lds<8>(ts, lane);
     if (want_fail) tile_to_lds<8>(tr, lane);
+#endif
     __syncthreads();
     const int ssh = ts.shift, rsh = tr.shift;
     const bool live = lane < ns;
