@@ -770,10 +770,12 @@ static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t str
         return (int)hipErrorInvalidValue;
     if (a.it1_lut && (!g.it1_vchk || !g.it1_cvar || g.m_pad != 64 * RC || g.n_pad != 64 * RV))
         return (int)hipErrorInvalidValue;
-    // the logicals, then the tile images, which the iteration-1 words reuse
-    const size_t tiles = 16 * (size_t)(((int64_t)64 * g.m + 15) / 16 + 2 + ((int64_t)64 * g.n_data + 15) / 16 + 2);
+    // the logicals, the tile images, the iteration-1 words (byte images: over
+    // the images; the kernel's layout, ms_triage_kernel)
+    const size_t tiles = triage_img_bytes(64 * (int64_t)g.m) + triage_img_bytes(64 * (int64_t)g.n_data);
+    const size_t it1 = a.it1_lut ? TriageIt1<RC, RV>::bytes : 0;
     const size_t lds = ((want_fail ? (size_t)g.k * g.lz_words * 8 : 0) + 15) / 16 * 16 +
-                       std::max(tiles, a.it1_lut ? TriageIt1<RC, RV>::bytes : (size_t)0);
+                       (QDEC_TRIAGE_BITS ? tiles + it1 : std::max(tiles, it1));
     if (lds > 64 * 1024) {  // large logical tables (k <= 256, lz_words <= 9)
         const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ms_triage_kernel<RC, RV>),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

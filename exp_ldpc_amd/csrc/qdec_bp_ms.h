@@ -753,16 +753,33 @@ __device__ __forceinline__ uint32_t byte_bits4(uint32_t d) { return ((d & 0x0101
 // One tile of a shot-major byte buffer, as the 16-B chunks covering bytes
 // [start, start + len) of a buffer of `total` bytes (image chunk 0 = the chunk
 // at or below `start`; `shift` = the byte offset of `start` inside the image).
+// QDEC_TRIAGE_BITS (default): the LDS image keeps only bit 0 of every byte
+// (16 bits per chunk, 1/8 of the bytes), so a tile pair needs ~3 KB of LDS
+// instead of ~21 KB and more tiles are in flight per CU; 0: byte images (A/B).
+#ifndef QDEC_TRIAGE_BITS
+#define QDEC_TRIAGE_BITS 1
+#endif
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+// bit 0 of 16 bytes as a 16-bit word (byte t -> bit t)
+__device__ __forceinline__ uint32_t chunk_bits16(u32x4 v) {
+    return byte_bits4(v.x) | (byte_bits4(v.y) << 4) | (byte_bits4(v.z) << 8) | (byte_bits4(v.w) << 12);
+}
 struct TileSrc {
     const uint8_t* buf;
     int64_t total, c0;  // c0: first 16-B chunk
     int nch, shift;
-    u32x4* img;
-    __device__ TileSrc(const uint8_t* b, int64_t tot, int64_t start, int64_t len, u32x4* dst) : buf(b), total(tot), img(dst) {
+    void* img;          // u32x4 per chunk, or u16 bits per chunk (QDEC_TRIAGE_BITS)
+    __device__ TileSrc(const uint8_t* b, int64_t tot, int64_t start, int64_t len, void* dst) : buf(b), total(tot), img(dst) {
         c0 = start >> 4;
         nch = (int)(((start + len + 15) >> 4) - c0);
         shift = (int)(start & 15);
+    }
+    __device__ __forceinline__ void put(int c, u32x4 v) const {
+#if QDEC_TRIAGE_BITS
+        static_cast<uint16_t*>(img)[c] = (uint16_t)chunk_bits16(v);
+#else
+        static_cast<u32x4*>(img)[c] = v;
+#endif
     }
     // chunk c of the image from its bytes (the buffer's last partial chunk)
     __device__ u32x4 bytes(int c) const {
@@ -797,7 +814,7 @@ __device__ __forceinline__ void tile_to_lds(const TileSrc& T, int lane) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = r0 + u * 64 + lane;
-            if (c < T.nch) T.img[c] = T.c0 + c < whole ? v[u] : T.bytes(c);
+            if (c < T.nch) T.put(c, T.c0 + c < whole ? v[u] : T.bytes(c));
         }
     }
 }
@@ -824,12 +841,12 @@ __device__ __forceinline__ void tile_pair_to_lds(const TileSrc& A, const TileSrc
 #pragma unroll
         for (int u = 0; u < UA; ++u) {
             const int c = ra + u * 64 + lane;
-            if (c < A.nch) A.img[c] = A.c0 + c < wa ? va[u] : A.bytes(c);
+            if (c < A.nch) A.put(c, A.c0 + c < wa ? va[u] : A.bytes(c));
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const int c = rb + u * 64 + lane;
-            if (c < B.nch) B.img[c] = B.c0 + c < wb ? vb[u] : B.bytes(c);
+            if (c < B.nch) B.put(c, B.c0 + c < wb ? vb[u] : B.bytes(c));
         }
     }
 }
@@ -914,6 +931,36 @@ __device__ __forceinline__ uint64_t lut4_words(uint32_t lut, uint64_t w0, uint64
     return f;
 }
 
+// The same from a bit image (QDEC_TRIAGE_BITS): bit `off` onwards, `len` bits;
+// reads up to three dwords past the row's last bit (the image has spares).
+template <int NW>
+__device__ __forceinline__ void row_bits_b(const uint32_t* img, int off, int len, uint64_t (&w)[NW]) {
+    const int q = off >> 5;
+    const uint32_t sh = (uint32_t)(off & 31);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        w[i] = 0ull;
+        if (64 * i < len) {  // uniform
+            const uint32_t d0 = img[q + 2 * i], d1 = img[q + 2 * i + 1], d2 = img[q + 2 * i + 2];
+            uint64_t v = (uint64_t)__builtin_amdgcn_alignbit(d1, d0, sh) |
+                         ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32);
+            if (64 * i + 64 > len) v &= (1ull << (len - 64 * i)) - 1ull;
+            w[i] = v;
+        }
+    }
+}
+
+// LDS bytes of a triage tile image of `len` bytes (plus the spares the row
+// readers run past its end)
+__host__ __device__ inline size_t triage_img_bytes(int64_t len) {
+    const int64_t nch = (len + 15) / 16 + 2;
+#if QDEC_TRIAGE_BITS
+    return (size_t)((2 * (nch + 8) + 15) / 16 * 16);
+#else
+    return (size_t)(16 * nch);
+#endif
+}
+
 // One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).
 template <int RC, int NWD>
 __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
@@ -937,8 +984,10 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     // row_bits reads one dword past a row)
     uint64_t* lz_lds = reinterpret_cast<uint64_t*>(smem);
     const int nlz = want_fail ? g.k * g.lz_words : 0;
-    u32x4* syn_img = reinterpret_cast<u32x4*>(smem + ((size_t)nlz * 8 + 15) / 16 * 16);
-    u32x4* rd_img = syn_img + (64 * m + 15) / 16 + 2;
+    unsigned char* syn_img = smem + ((size_t)nlz * 8 + 15) / 16 * 16;
+    unsigned char* rd_img = syn_img + triage_img_bytes(64 * (int64_t)m);
+    // iteration-1 words: past the images (bit images), over them (byte images)
+    unsigned char* it1_base = QDEC_TRIAGE_BITS ? rd_img + triage_img_bytes(64 * (int64_t)nd) : syn_img;
     for (int e = lane; e < nlz; e += 64) lz_lds[e] = g.lz[e];
     // iteration-1 tables (TriageIt1), loaded ahead of the tiles
     uint64_t it_ids[NWD], it_cv[RC][2];
@@ -970,11 +1019,19 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     const bool live = lane < ns;
     const int64_t shot = s0 + lane;
     uint64_t sw[RC];
+#if QDEC_TRIAGE_BITS
+    row_bits_b<RC>(reinterpret_cast<const uint32_t*>(syn_img), ssh + lane * m, m, sw);
+#else
     row_bits<RC>(reinterpret_cast<const uint32_t*>(syn_img), ssh + lane * m, m, sw);
+#endif
     uint64_t rp[kMaxLogicalRounds] = {0ull, 0ull, 0ull, 0ull};
     if (want_fail) {
         uint64_t rw[NWD];
+#if QDEC_TRIAGE_BITS
+        row_bits_b<NWD>(reinterpret_cast<const uint32_t*>(rd_img), rsh + lane * nd, nd, rw);
+#else
         row_bits<NWD>(reinterpret_cast<const uint32_t*>(rd_img), rsh + lane * nd, nd, rw);
+#endif
         for (int r = 0; r < g.k; ++r) {  // uniform rows of the dense logical table (LDS broadcasts)
             int par = 0;
 #pragma unroll
@@ -994,9 +1051,9 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     for (int rc = 0; rc < RC; ++rc) wt += __popcll(sw[rc]);
     const bool it1 = a.it1_lut && __popcll(__ballot(live && wt <= 12)) >= 8;
     if (it1) {  // uniform: iteration 1 here (TriageIt1)
-        // in the tile images' place (dead once the rows are bit words)
+        // (byte images: in their place, dead once the rows are bit words)
         wave_lds_sync();
-        uint64_t* synT = reinterpret_cast<uint64_t*>(syn_img);
+        uint64_t* synT = reinterpret_cast<uint64_t*>(it1_base);
         uint64_t* xT = synT + RC * 64 + 1;
         uint64_t* lzp = xT + NWD * 64 + 1;
         // transpose: lane t gets the word of check rc * 64 + t
