@@ -33,6 +33,8 @@ for p in [float(x) for x in (sys.argv[1:] or ["0.001", "0.1"])]:
             torch.cuda.synchronize()
             lib.qd_dev_read_stamps(buf.ctypes.data, 64, 1)
             shots = int(buf[9]); its = int(buf[8])
+            if not shots:  # the compact path's kernels stamp other slots (stamps_cmp.py)
+                continue
             print(f"p={p} {label} ssf={int(ssf)} shots={shots} iters/shot={its/shots:.2f} cycles/shot: " +
                   " ".join(f"{n}={buf[i]/shots:.0f}" for i, n in enumerate(names)) +
                   f" | per-iter={buf[2]/its:.0f} | waves={int(buf[12])} ticks/wave={buf[10]/max(1,buf[12]):.0f}"
