@@ -886,6 +886,9 @@ struct TriageIt1 {
     static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
 };
 
+#ifndef QDEC_TRIAGE_UB
+#define QDEC_TRIAGE_UB 16  // readout-tile loads per lane per round (A/B)
+#endif
 #ifndef QDEC_TRIAGE_PAIR
 #define QDEC_TRIAGE_PAIR 1  // 0: the syndrome tile, then the readout tile (A/B)
 #endif
@@ -962,8 +965,11 @@ __host__ __device__ inline size_t triage_img_bytes(int64_t len) {
 }
 
 // One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).
+#ifndef QDEC_TRIAGE_OCC
+#define QDEC_TRIAGE_OCC 1  // waves per SIMD the triage's registers are budgeted for (A/B)
+#endif
 template <int RC, int NWD>
-__global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
     using Ent = CmpEntry<RC>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -1008,7 +1014,8 @@ __global__ __launch_bounds__(64) void ms_triage_kernel(DevGraph g, DecodeArgs a)
     const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
                      want_fail ? (int64_t)ns * nd : 0, rd_img);
 #if QDEC_TRIAGE_PAIR
-    if (want_fail) tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < 16 ? 4 * NWD : 16)>(ts, tr, lane);
+    if (want_fail)
+        tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < QDEC_TRIAGE_UB ? 4 * NWD : QDEC_TRIAGE_UB)>(ts, tr, lane);
     else tile_to_lds<8>(ts, lane);
 #else
     tile_to_lds<8>(ts, lane);
