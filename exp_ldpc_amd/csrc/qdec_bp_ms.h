@@ -886,6 +886,12 @@ struct TriageIt1 {
     static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
 };
 
+#ifndef QDEC_T1_GATE_W
+#define QDEC_T1_GATE_W 12  // iteration-1 tile gate: syndrome weight bound ...
+#endif
+#ifndef QDEC_T1_GATE_N
+#define QDEC_T1_GATE_N 8  // ... and shots of the tile within it (A/B defines)
+#endif
 #ifndef QDEC_TRIAGE_UB
 #define QDEC_TRIAGE_UB 16  // readout-tile loads per lane per round (A/B)
 #endif
@@ -1056,7 +1062,7 @@ __global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph
     int wt = 0;
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc) wt += __popcll(sw[rc]);
-    const bool it1 = a.it1_lut && __popcll(__ballot(live && wt <= 12)) >= 8;
+    const bool it1 = a.it1_lut && __popcll(__ballot(live && wt <= QDEC_T1_GATE_W)) >= QDEC_T1_GATE_N;
     if (it1) {  // uniform: iteration 1 here (TriageIt1)
         // (byte images: in their place, dead once the rows are bit words)
         wave_lds_sync();
