@@ -75,6 +75,10 @@ SIGNATURES = {
     "qd_graph_last_kernels": (_i32, [_p, C.c_char_p, _i32, C.c_char_p, _i32, C.c_char_p, _i32]),
     "qd_osd_device_supported": (_i32, [_p]),
     "qd_osd_batch_device": (_i32, [_p, _i32, _i32, _i64, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "qd_graph_set_option": (_i32, [_p, _i32, _i32]),
+    "qd_graph_get_option": (_i32, [_p, _i32, C.POINTER(_i32)]),
+    "qd_graph_ssf_tables": (_i32, [_p, C.POINTER(_i32), C.POINTER(_i64)]),
+    "qd_graph_ssf_tables_copy": (_i32, [_p, _p, _p, _p, _p, C.POINTER(_i32), C.POINTER(_i32)]),
     "qd_gf2_rref": (_i64, [_p, _i64, _i64, _i64, _p, _i32]),
     "qd_gf2_extend_basis": (_i64, [_p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64]),
 }

@@ -230,7 +230,7 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
         // f64: the transfer of a ds_write_b64 takes 6 cycles but every array
         // cycle beyond 4 is a bank-conflict cycle the CU's other waves wait
         // for (PMC: the array is the busiest unit), so the floor is 4
-        static const bool v1 = std::getenv("QDEC_MS_LAYOUT_V1") != nullptr;  // A/B: round-2 layout
+        constexpr bool v1 = false;  // round-2 layout (tools/dev/patches/r05_pruned_knobs.patch restores the switch)
         const int ngl = p == 1 ? 2 : 4, ncl = p == 1 ? 32 : 16, floor_c = p == 1 ? 4 : (v1 ? 6 : 4);
         const int lanes_per = 64 / ngl;
         std::vector<int> grp(E), lg(E), pos(E);
@@ -874,8 +874,7 @@ DecodeArgs make_args(const qd_graph* g, const qd_params* p, int64_t B, const uin
     if (!syn && !(a.syn_flags && (base || readout))) throw Fail(-7, "no syndrome source");
     if (!g->ctl) hip_check(hipMalloc(&const_cast<qd_graph*>(g)->ctl, 256), "hipMalloc control block");
     a.wave_ctr = static_cast<unsigned long long*>(g->ctl);
-    const char* ns = std::getenv("QDEC_SSF_NOSPLIT");
-    a.ssf_nosplit = (ns && ns[0] == '1') ? 1 : 0;
+    a.ssf_nosplit = g->dg.opt_ssf == kSsfScanNoSplit ? 1 : 0;
     return a;
 }
 
@@ -934,6 +933,7 @@ int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t*
             G->dg.n_gen = 0;
             G->dg.g_inv = nullptr;
             G->dg.g_invd = G->dg.g_invl = 0;
+            default_options(G->dg);
         } catch (...) {
             G->arena.release();
             if (G->stream) (void)hipStreamDestroy(G->stream);
@@ -979,6 +979,7 @@ int qd_graph_create_host(int32_t m, int32_t n, const int32_t* row_ptr, const int
             G->dg.n_gen = 0;
             G->dg.g_inv = nullptr;
             G->dg.g_invd = G->dg.g_invl = 0;
+            default_options(G->dg);
         } catch (...) {
             delete G;
             throw;
@@ -1028,6 +1029,114 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->stream) (void)hipStreamDestroy(g->stream);
         delete g;
     });
+}
+
+// Tables of the table-driven SSF kernel (ssf_lut_kernel, qdec_bp.hip; the s_*
+// fields of DevGraph).  Inside one generator the spec's choice depends only on
+// its local syndrome sl (the residual restricted to the checks its qubits
+// touch): the best score max_t gain(t) * 840 / |t| over the non-empty subsets t,
+// gain(t) = popc(sl) - popc(sl ^ M_t), and the lowest t reaching it (the
+// oracle's strict-improvement scan in ascending t, oracle/qdec_oracle.c
+// ssf_run).  One table over sl therefore replaces the per-step subset search,
+// and generators whose qubits meet their local checks in the same pattern share
+// it: local checks are ordered by signature (the bitmask of the generator's
+// qubit positions touching them, ties by check id), which makes the masks M_t
+// of two such generators identical (every generator of a hypergraph product
+// code has the same 4 x 3 pattern).  Qualifies with <= 128 generators, m_pad <=
+// 255 (u8 check ids), <= kLutLC local checks per generator, <= 255 distinct
+// positive scores and tables within kLutBudget bytes of LDS; otherwise the s_*
+// pointers stay null and the scanning kernel (ssf_wave_kernel) runs.
+constexpr size_t kLutBudget = 96 * 1024;
+static void ssf_lut_tables(qd_graph* G, int n_gen, const int32_t* gen_ptr, const int32_t* gen_idx, int gp) {
+    DevGraph& g = G->dg;
+    g.s_lut = g.s_off = g.s_lcw = g.s_tog = nullptr;
+    g.s_lut_n = 0;
+    if (n_gen > 128 || g.m_pad > 255) return;
+    std::vector<std::vector<uint32_t>> shapes;  // (w, nlc, M_0 .. M_{w-1}) in first-seen order
+    std::vector<int> shape_off;
+    std::vector<uint32_t> off(gp, 0);
+    std::vector<uint32_t> lcw((size_t)kLutLCW * gp, 0xffffffffu);
+    std::vector<uint32_t> tog((size_t)g.m_pad * 64, 0);
+    int total = 0;
+    for (int gi = 0; gi < n_gen; ++gi) {
+        const int a = gen_ptr[gi], w = gen_ptr[gi + 1] - a;
+        std::vector<std::pair<int, uint32_t>> sig;  // (check, signature)
+        for (int k = 0; k < w; ++k) {
+            const int q = gen_idx[a + k];
+            for (int t = G->col_ptr[q]; t < G->col_ptr[q + 1]; ++t) {
+                const int c = G->col_rows[t];
+                auto it = std::find_if(sig.begin(), sig.end(), [c](const auto& e) { return e.first == c; });
+                if (it == sig.end()) sig.push_back({c, 1u << k});
+                else it->second ^= 1u << k;
+            }
+        }
+        if ((int)sig.size() > kLutLC) return;
+        std::sort(sig.begin(), sig.end(), [](const auto& x, const auto& y) {
+            return x.second != y.second ? x.second < y.second : x.first < y.first;
+        });
+        const int nlc = (int)sig.size();
+        std::vector<uint32_t> key = {(uint32_t)w, (uint32_t)nlc};
+        for (int k = 0; k < w; ++k) {
+            uint32_t mk = 0;
+            for (int b = 0; b < nlc; ++b)
+                if ((sig[b].second >> k) & 1) mk |= 1u << b;
+            key.push_back(mk);
+        }
+        const auto it = std::find(shapes.begin(), shapes.end(), key);
+        int o;
+        if (it == shapes.end()) {
+            o = total;
+            shapes.push_back(key);
+            shape_off.push_back(o);
+            total += 1 << nlc;
+        } else {
+            o = shape_off[it - shapes.begin()];
+        }
+        off[gi] = (uint32_t)o;
+        for (int b = 0; b < nlc; ++b) {
+            const int c = sig[b].first;
+            uint32_t& word = lcw[(size_t)(b / 4) * gp + gi];
+            word = (word & ~(0xffu << (8 * (b % 4)))) | ((uint32_t)c << (8 * (b % 4)));
+            tog[(size_t)c * 64 + (gi & 63)] |= (1u << b) << (16 * (gi >> 6));
+        }
+    }
+    if ((size_t)total * 4 + (size_t)g.m_pad * 256 > kLutBudget) return;
+    // best (score, t) of every local syndrome of every shape; scores -> ranks
+    std::vector<int> score(total, 0);
+    std::vector<uint32_t> lut(total, 0);
+    for (size_t s = 0; s < shapes.size(); ++s) {
+        const int w = (int)shapes[s][0], nlc = (int)shapes[s][1], o = shape_off[s];
+        std::vector<uint32_t> Mt((size_t)1 << w, 0);
+        for (int t = 1; t < (1 << w); ++t) Mt[t] = Mt[t & (t - 1)] ^ shapes[s][2 + __builtin_ctz(t)];
+        for (int sl = 0; sl < (1 << nlc); ++sl) {
+            const int base = __builtin_popcount(sl);
+            int best = 0, bt = 0;
+            for (int t = 1; t < (1 << w); ++t) {
+                const int gain = base - __builtin_popcount((uint32_t)sl ^ Mt[t]);
+                if (gain <= 0) continue;
+                const int sc = gain * kSsfScale / __builtin_popcount(t);
+                if (sc > best) {  // strict: ties keep the lowest t
+                    best = sc;
+                    bt = t;
+                }
+            }
+            score[o + sl] = best;
+            lut[o + sl] = bt ? (Mt[bt] << 8 | (uint32_t)bt) : 0u;
+        }
+    }
+    std::vector<int> ranks(score.begin(), score.end());
+    std::sort(ranks.begin(), ranks.end());
+    ranks.erase(std::unique(ranks.begin(), ranks.end()), ranks.end());
+    if (!ranks.empty() && ranks[0] == 0) ranks.erase(ranks.begin());
+    if (ranks.size() > 255) return;
+    for (int e = 0; e < total; ++e)
+        if (score[e] > 0)
+            lut[e] |= (uint32_t)(std::lower_bound(ranks.begin(), ranks.end(), score[e]) - ranks.begin() + 1) << 24;
+    g.s_lut = G->flip_arena.upload(lut);
+    g.s_lut_n = total;
+    g.s_off = G->flip_arena.upload(off);
+    g.s_lcw = G->flip_arena.upload(lcw);
+    g.s_tog = G->flip_arena.upload(tog);
 }
 
 int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, const int32_t* gen_idx) {
@@ -1090,11 +1199,10 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         while ((size_t)1 << invl < invmax) ++invl;
         const int invd = 1 << invl;
         std::vector<uint16_t> invt;
-        // QDEC_SSF_GATHER=1: no inverse table, the wave SSF kernel re-gathers the
-        // local syndromes every step (the path of graphs whose table is too wide)
-        const char* gather_env = std::getenv("QDEC_SSF_GATHER");
-        const bool gather = gather_env && gather_env[0] == '1';
-        if (pack8 && n_gen <= 128 && invd <= 64 && !gather) {
+        // graphs whose table would be too wide get none: the scanning wave SSF
+        // kernel then re-gathers the local syndromes every step (QD_SSF_SCAN_GATHER
+        // takes that path on any graph)
+        if (pack8 && n_gen <= 128 && invd <= 64) {
             invt.assign((size_t)g.m_pad * invd, 0xffff);
             for (int i = 0; i < g.m_pad; ++i)
                 for (size_t t = 0; t < inv[i].size(); ++t) invt[(size_t)i * invd + t] = inv[i][t];
@@ -1111,6 +1219,7 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
         g.g_qmask = G->flip_arena.upload(qm);
         if (pack8) g.g_lc8 = G->flip_arena.upload(lc8);
         g.g_nlcmax = nlcmax;
+        ssf_lut_tables(G, n_gen, gen_ptr, gen_idx, gp);
         g.g_iptr = nullptr;
         g.g_ient = nullptr;
         if (n_gen < 65536) {
@@ -1513,6 +1622,73 @@ int qd_graph_last_kernels(qd_graph* G, char* bp, int32_t bp_len, char* ssf, int3
         put(G->last_bp, bp, bp_len);
         put(G->last_ssf, ssf, ssf_len);
         put(G->last_pre, pre, pre_len);
+    });
+}
+
+int qd_graph_set_option(qd_graph* G, int32_t option, int32_t value) {
+    return guarded([&] {
+        check_graph(G);
+        DevGraph& g = G->dg;
+        auto in = [&](int lo, int hi) {
+            if (value < lo || value > hi) throw Fail(-2, "option value out of range");
+        };
+        switch (option) {
+            case QD_OPT_COMPACT: in(0, 1); g.opt_compact = value; break;
+            case QD_OPT_TRIAGE_IT1: in(0, 1); g.opt_triage_it1 = value; break;
+            case QD_OPT_SSF: in(QD_SSF_AUTO, QD_SSF_SCAN_NOSPLIT); g.opt_ssf = value; break;
+            case QD_OPT_LDS_KERNEL: in(-1, 1); g.opt_lds_kernel = value; break;
+            case QD_OPT_GROUP_KERNEL: in(-1, 1); g.opt_group_kernel = value; break;
+            case QD_OPT_SSF_INC: in(0, 1); g.opt_ssf_inc = value; break;
+            case QD_OPT_BLOCK_WG: in(0, 64); g.opt_block_wg = value; break;
+            case QD_OPT_GROUP_MB: in(0, 1 << 22); g.opt_group_mb = value; break;
+            default: throw Fail(-2, "unknown option");
+        }
+    });
+}
+
+int qd_graph_get_option(const qd_graph* G, int32_t option, int32_t* value) {
+    return guarded([&] {
+        check_graph(G);
+        if (!value) throw Fail(-1, "null output");
+        const DevGraph& g = G->dg;
+        switch (option) {
+            case QD_OPT_COMPACT: *value = g.opt_compact; break;
+            case QD_OPT_TRIAGE_IT1: *value = g.opt_triage_it1; break;
+            case QD_OPT_SSF: *value = g.opt_ssf; break;
+            case QD_OPT_LDS_KERNEL: *value = g.opt_lds_kernel; break;
+            case QD_OPT_GROUP_KERNEL: *value = g.opt_group_kernel; break;
+            case QD_OPT_SSF_INC: *value = g.opt_ssf_inc; break;
+            case QD_OPT_BLOCK_WG: *value = g.opt_block_wg; break;
+            case QD_OPT_GROUP_MB: *value = g.opt_group_mb; break;
+            default: throw Fail(-2, "unknown option");
+        }
+    });
+}
+
+int qd_graph_ssf_tables(const qd_graph* G, int32_t* has_lut, int64_t* lut_bytes) {
+    return guarded([&] {
+        check_graph(G);
+        if (has_lut) *has_lut = G->dg.s_lut ? 1 : 0;
+        if (lut_bytes) *lut_bytes = G->dg.s_lut ? (int64_t)G->dg.s_lut_n * 4 : 0;
+    });
+}
+
+int qd_graph_ssf_tables_copy(const qd_graph* G, uint32_t* lut, uint32_t* off, uint32_t* lcw, uint32_t* tog,
+                             int32_t* g_pad, int32_t* m_pad) {
+    return guarded([&] {
+        check_graph(G);
+        if (!G->host_only) throw Fail(-16, "table copies are kept for host-only graphs (qd_graph_create_host)");
+        const DevGraph& g = G->dg;
+        if (!g.s_lut) throw Fail(-36, "the graph has no table-driven SSF tables");
+        if (g_pad) *g_pad = g.g_pad;
+        if (m_pad) *m_pad = g.m_pad;
+        auto put = [](uint32_t* dst, const uint32_t* src, size_t n) {
+            if (dst) std::memcpy(dst, src, n * 4);
+        };
+        put(lut, g.s_lut, (size_t)g.s_lut_n);
+        put(off, g.s_off, (size_t)g.g_pad);
+        put(lcw, g.s_lcw, (size_t)kLutLCW * g.g_pad);
+        put(tog, g.s_tog, (size_t)g.m_pad * 64);
     });
 }
 

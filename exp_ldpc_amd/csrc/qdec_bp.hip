@@ -673,6 +673,216 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
     QDEC_FLUSH_AT(16);
 }
 
+// ============================================================== SSF, table-driven
+// ssf_lut_kernel: the same spec as ssf_wave_kernel with the per-generator subset
+// search replaced by one LDS table lookup (DevGraph::s_lut, built by
+// ssf_lut_tables in qdec_abi.cpp): the best (score, subset) of a generator is a
+// function of its <= 16-bit local syndrome.  One wave per queued shot; lane l
+// owns generators l and 64 + l, whose local syndromes it keeps in registers
+// (one u32: generator l in the low half-word).  A step is
+//   1. two table reads -> key (rank, -g, t) per generator, a DPP wave max;
+//   2. the winner's entry and local syndrome from its owner lane (readlane);
+//   3. for every check the flip toggles, one coalesced read of that check's
+//      toggle row (s_tog: the local-syndrome bits of every lane's generators),
+//      XORed into the registers; lanes k < 8 toggle the hard-decision byte of
+//      the winner's qubit k when it is in the subset (qubit ids from an LDS
+//      table; nothing waits for these writes until the shot's end).
+// Two dependent LDS round trips per step and no LDS writes, against the scanning
+// kernel's gather / list / score / pick / apply chain.  The shot's first local
+// syndromes are the toggle rows of its residual's violated checks.
+constexpr int kLutWaves = 16;  // waves per workgroup sharing the tables
+#ifndef QDEC_LUT_OCC
+#define QDEC_LUT_OCC 8         // waves per SIMD the table-driven kernel is compiled for
+#endif
+
+struct SsfLutLds {
+    static constexpr int kStage = 3;  // packed queue entries staged per wave (two slots ahead)
+    __host__ __device__ static size_t lut_bytes(const DevGraph& g) { return ((size_t)g.s_lut_n * 4 + 15) / 16 * 16; }
+    __host__ __device__ static size_t tog_bytes(const DevGraph& g) { return (size_t)g.m_pad * 64 * 4; }
+    __host__ __device__ static size_t lz_bytes(const DevGraph& g) {
+        return lz_in_lds(g) ? ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16 : 0;
+    }
+    static constexpr size_t qt_bytes = (size_t)(kGenW / 2) * 128 * 4;  // qubit id pairs [kGenW/2][128]
+    __host__ __device__ static size_t shared_bytes(const DevGraph& g) {
+        return lut_bytes(g) + tog_bytes(g) + qt_bytes + lz_bytes(g);
+    }
+    // staged queue entries, hard decision bytes
+    __host__ __device__ static size_t wave_bytes(const DevGraph& g) {
+        return 256 * kStage + ((size_t)g.n_pad + 64 + 15) / 16 * 16;
+    }
+};
+
+// LEAN: outputs are status, SSF steps and the failure flag only (the bench's and
+// p_sweep's call); otherwise finalize_shot writes x / corr (its registers would
+// push the lean build past 64 VGPRs, 8 waves per SIMD).
+template <int RG, int XW, int RW, bool LEAN>
+__global__ __launch_bounds__(64 * kLutWaves, LEAN ? QDEC_LUT_OCC : 4) void ssf_lut_kernel(DevGraph g, DecodeArgs a) {
+    static_assert(RG == 1 || RG == 2, "two generators per lane at most (16-bit halves of one word)");
+    static_assert(XW <= 32, "hard-decision bits per lane");
+    constexpr int QW = QEntry<XW, RW>::QW;
+    static_assert(2 * QW <= 64, "entry staging");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* lut = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* tog = reinterpret_cast<uint32_t*>(smem + SsfLutLds::lut_bytes(g));
+    uint32_t* qt = reinterpret_cast<uint32_t*>(smem + SsfLutLds::lut_bytes(g) + SsfLutLds::tog_bytes(g));
+    uint64_t* lzs = reinterpret_cast<uint64_t*>(smem + SsfLutLds::lut_bytes(g) + SsfLutLds::tog_bytes(g) +
+                                                SsfLutLds::qt_bytes);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned char* wbase = smem + SsfLutLds::shared_bytes(g) + (size_t)wave * SsfLutLds::wave_bytes(g);
+    uint8_t* ent = wbase;                                  // [kStage][256] queue entries
+    uint8_t* xh = wbase + 256 * SsfLutLds::kStage;         // [n_pad + 64] hard decision
+
+    {   // tables -> LDS, 16-B copies (every size is a multiple of 16 B)
+        const uint4* src = reinterpret_cast<const uint4*>(g.s_lut);
+        uint4* dst = reinterpret_cast<uint4*>(lut);
+        const int nl = (int)(SsfLutLds::lut_bytes(g) / 16);
+        for (int e = threadIdx.x; e < nl; e += 64 * kLutWaves) dst[e] = src[e];
+        src = reinterpret_cast<const uint4*>(g.s_tog);
+        dst = reinterpret_cast<uint4*>(tog);
+        const int nt = (int)(SsfLutLds::tog_bytes(g) / 16);
+        for (int e = threadIdx.x; e < nt; e += 64 * kLutWaves) dst[e] = src[e];
+    }
+    if (lz_in_lds(g))
+        for (int e = threadIdx.x; e < g.k * g.lz_words; e += 64 * kLutWaves) lzs[e] = g.lz[e];
+    for (int e = threadIdx.x; e < 64 * RG; e += 64 * kLutWaves)
+#pragma unroll
+        for (int k = 0; k < kGenW / 2; ++k)
+            qt[k * 128 + e] = (uint32_t)g.g_q[(2 * k) * g.g_pad + e] | ((uint32_t)g.g_q[(2 * k + 1) * g.g_pad + e] << 16);
+    for (int e = lane; e < g.n_pad + 64; e += 64) xh[e] = 0;
+    // this lane's generators: table offsets, canonical local checks
+    uint32_t off[RG], lcw[RG][kLutLCW];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+        const int gi = rg * 64 + lane;
+        off[rg] = g.s_off[gi];
+#pragma unroll
+        for (int w = 0; w < kLutLCW; ++w) lcw[rg][w] = g.s_lcw[w * g.g_pad + gi];
+    }
+    __syncthreads();
+
+    const int count = *a.q_count;
+    auto stage_entry = [&](int sl, int b) {  // as ssf_wave_kernel: one LDS-DMA load per stage
+        const int64_t e = sl < count ? sl : 0;
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(a.q_w + e * QW) + 4 * min(lane, 2 * QW - 1);
+        __builtin_amdgcn_global_load_lds(src, ent + 256 * b, 4, 0, 0);
+    };
+    const int stride = gridDim.x * kLutWaves;
+    const bool lean_fin = LEAN;
+    const bool want_fail = a.fail && a.readout && g.k > 0;
+    const bool rpar = a.q_rpar != 0;
+    unsigned long long* sctr = a.wave_ctr && count >= 16 * stride ? a.wave_ctr + 1 : nullptr;
+    ShotSeq seq(count, sctr, (int64_t)blockIdx.x * kLutWaves + wave, stride, lane);
+    int64_t slot = seq.next(lane);
+    int64_t slot1 = seq.next(lane);
+    stage_entry((int)min(slot, (int64_t)count), 0);
+    stage_entry((int)min(slot1, (int64_t)count), 1);
+    int sb = 0;
+    for (; slot < count; sb = sb == 2 ? 0 : sb + 1) {
+        wait_vmem<1>();
+        const uint64_t* ew = reinterpret_cast<const uint64_t*>(ent + 256 * sb);
+        const int64_t shot = (int64_t)ew[0];
+#pragma unroll
+        for (int w = 0; w < XW; ++w) xh[w * 64 + lane] = (uint8_t)((ew[1 + w] >> lane) & 1);
+        uint64_t R[RW];  // residual words (uniform)
+#pragma unroll
+        for (int w = 0; w < RW; ++w) {
+            const uint64_t v = ew[1 + XW + w];
+            R[w] = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+        }
+        wait_lds();
+        const int64_t slot2 = seq.next(lane);
+        stage_entry((int)min(slot2, (int64_t)count), sb == 0 ? 2 : sb - 1);
+        // first local syndromes: the toggle rows of the violated checks
+        uint32_t sl = 0;
+        int sw = 0;
+#pragma unroll
+        for (int w = 0; w < RW; ++w) {
+            uint64_t bits = R[w];
+            sw += __popcll(bits);
+            while (bits) {
+                const int c = w * 64 + __builtin_ctzll(bits);
+                bits &= bits - 1;
+                sl ^= tog[c * 64 + lane];
+            }
+        }
+        int steps = 0;
+        while (sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
+            // ---- 1. every generator's best (rank, -g, t); wave max ----
+            uint32_t e[RG];
+            int kv = 0;
+#pragma unroll
+            for (int rg = 0; rg < RG; ++rg) {
+                const uint32_t s = rg ? (sl >> 16) : (sl & 0xffffu);
+                e[rg] = lut[off[rg] + s];
+                const uint32_t rank = e[rg] >> 24;
+                const int key = rank ? (int)((rank << 15) | ((uint32_t)(127 - (rg * 64 + lane)) << 8) | (e[rg] & 0xffu)) : 0;
+                kv = max(kv, key);
+            }
+            const int best = wave_max_i32(kv);
+            if (best == 0) break;  // no positive gain left
+            const int gsel = 127 - ((best >> 8) & 127);
+            const int tsel = best & 255;
+            const int owner = gsel & 63;
+            const bool hi = RG == 2 && gsel >= 64;
+            // ---- 2. the winner's toggled checks and gain (owner lane) ----
+            const uint32_t esel = (uint32_t)__builtin_amdgcn_readlane((int)(hi ? e[RG - 1] : e[0]), owner);
+            const uint32_t slg = ((uint32_t)__builtin_amdgcn_readlane((int)sl, owner) >> (hi ? 16 : 0)) & 0xffffu;
+            const uint32_t fm = (esel >> 8) & 0xffffu;
+            sw -= __builtin_popcount(slg) - __builtin_popcount(slg ^ fm);
+            ++steps;
+            // ---- 3. toggle the flipped checks' local-syndrome bits, flip the qubits ----
+#pragma unroll
+            for (int w = 0; w < kLutLCW; ++w) {
+                uint32_t bits = (fm >> (4 * w)) & 0xfu;
+                if (bits) {
+                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)(hi ? lcw[RG - 1][w] : lcw[0][w]), owner);
+                    do {
+                        const int b = __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        sl ^= tog[((word >> (8 * b)) & 0xffu) * 64 + lane];
+                    } while (bits);
+                }
+            }
+            if (lane < kGenW && ((tsel >> lane) & 1)) {
+                const uint32_t pair = qt[(lane >> 1) * 128 + gsel];
+                xh[(pair >> (16 * (lane & 1))) & 0xffffu] ^= 1;
+            }
+        }
+        wave_lds_sync();
+        if (lean_fin) {
+            uint64_t X[XW];
+#pragma unroll
+            for (int w = 0; w < XW; ++w) X[w] = __ballot(xh[w * 64 + lane] & 1);
+            int any_fail = 0;
+            if (want_fail) {  // the entry carries the readout words or (q_rpar) its logical parities
+                uint64_t Rd[XW];
+#pragma unroll
+                for (int w = 0; w < XW; ++w) Rd[w] = X[w] ^ (rpar ? 0ull : ew[1 + XW + RW + w]);
+                int f = 0;
+#pragma unroll
+                for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                    const int r = rr * 64 + lane;
+                    if (r < g.k)
+                        f |= lz_row_parity<XW>(g, lzs, r, Rd) ^
+                             (rpar && rr < XW ? (int)((ew[1 + XW + RW + (rr < XW ? rr : 0)] >> lane) & 1) : 0);
+                }
+                any_fail = __ballot(f) != 0ull;
+            }
+            if (lane == 0) {
+                if (a.status) a.status[shot] = (uint8_t)(sw == 0 ? 2 : 0);
+                if (a.ssf_steps) a.ssf_steps[shot] = steps;
+                if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+            }
+        } else {
+            if constexpr (!LEAN) finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
+        }
+        wave_lds_sync();
+        slot = slot1;
+        slot1 = slot2;
+    }
+}
+
 // ---------------------------------------------------------------- launcher
 LaunchNames& last_launch_names() {
     static thread_local LaunchNames n;
@@ -711,6 +921,38 @@ static int launch_ssf_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, 
     return (int)hipGetLastError();
 }
 
+template <int RG, int XW, int RW, bool LEAN>
+static int launch_ssf_lut_t(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    const size_t lds = SsfLutLds::shared_bytes(g) + kLutWaves * SsfLutLds::wave_bytes(g);
+    if (lds > 160 * 1024) return (int)hipErrorInvalidConfiguration;
+    if (lds > 64 * 1024) {
+        const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ssf_lut_kernel<RG, XW, RW, LEAN>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return (int)ea;
+    }
+    int per_cu = 0;
+    hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ssf_lut_kernel<RG, XW, RW, LEAN>, 64 * kLutWaves, lds);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    long long grid = (long long)num_cus * per_cu;
+    const long long need = (a.B + kLutWaves - 1) / kLutWaves;  // queue length <= B
+    if (grid > need) grid = need;
+    if (grid <= 0) return 0;
+    QDEC_NOTE_SSF("qdec::ssf_lut_kernel", RG, XW, RW, LEAN);
+    hipLaunchKernelGGL((ssf_lut_kernel<RG, XW, RW, LEAN>), dim3((unsigned)grid), dim3(64 * kLutWaves), lds, stream, g,
+                       a);
+    return (int)hipGetLastError();
+}
+
+template <int RG, int XW, int RW>
+static int launch_ssf_lut(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    if (a.fail && g.k > 0 && !g.lz) return (int)hipErrorInvalidValue;
+    const bool lean = !a.x_out && !a.corr_out && !a.base && g.fold_blocks == 1;
+    return lean ? launch_ssf_lut_t<RG, XW, RW, true>(g, a, num_cus, stream)
+                : launch_ssf_lut_t<RG, XW, RW, false>(g, a, num_cus, stream);
+}
+
 template <typename K>
 static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, const DevGraph& g,
                              const DecodeArgs& a, int block = 64, int max_per_cu = 0) {
@@ -723,11 +965,6 @@ static int launch_persistent(K kern, size_t lds, int64_t work, int num_cus, hipS
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
-    static const int cap = [] {  // diagnostics: QDEC_MAX_BLOCKS_PER_CU caps the persistent grid
-        const char* v = std::getenv("QDEC_MAX_BLOCKS_PER_CU");
-        return v ? std::atoi(v) : 0;
-    }();
-    if (cap > 0 && per_cu > cap) per_cu = cap;
     if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
     // one-wave blocks: a multiple of 4 per CU puts the same number of waves on
     // every SIMD (11 f64 waves would sit 3/3/3/2 and run slower than 8)
@@ -756,10 +993,8 @@ static bool compact_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
     if ((reinterpret_cast<uintptr_t>(a.syn) & 15) || (a.readout && (reinterpret_cast<uintptr_t>(a.readout) & 15)))
         return false;
     if ((reinterpret_cast<uintptr_t>(a.cmp_count) & 127) || (reinterpret_cast<uintptr_t>(a.cmp) & 15)) return false;
-    const char* v = std::getenv("QDEC_COMPACT");  // read per launch: tests switch it within a process
-    const bool off = v && v[0] == '0';
     const bool want_fail = a.fail && a.readout && g.k > 0;
-    return !off && a.cmp && a.cmp_count && a.syn && lean_launch(g, a, defer) && (!want_fail || g.ms_lzs);
+    return g.opt_compact && a.cmp && a.cmp_count && a.syn && lean_launch(g, a, defer) && (!want_fail || g.ms_lzs);
 }
 
 template <int RC, int RV>
@@ -807,9 +1042,8 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             DecodeArgs b = a;
             b.cmp_zero_ok = (g.ms_allpos >> (sizeof(T) == 4 ? 1 : 0)) & 1;
             // iteration 1 in the triage: the tables assume alpha_1 = 0.5 (the
-            // default schedule); QDEC_TRIAGE_IT1=0 leaves it to the BP kernel (A/B)
-            const char* it1_env = std::getenv("QDEC_TRIAGE_IT1");
-            b.it1_lut = (a.ms_scaling == 0.0 && a.max_iter >= 1 && !(it1_env && it1_env[0] == '0'))
+            // default schedule); QD_OPT_TRIAGE_IT1 = 0 leaves it to the BP kernel
+            b.it1_lut = (a.ms_scaling == 0.0 && a.max_iter >= 1 && g.opt_triage_it1)
                             ? g.it1_lut[sizeof(T) == 4 ? 1 : 0]
                             : nullptr;
             hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpSegs * 128, stream);
@@ -820,9 +1054,8 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             // a capped grid (f64: 8 waves per CU) must also be placed evenly: the
             // dispatcher stacks up to the kernel's own occupancy on a CU (11 for
             // the 159-VGPR f64 kernel) while others sit idle, so the LDS request is
-            // padded to 1/cap of the CU (QDEC_CMP_LDS_PAD=0: unpadded, A/B)
-            const char* pad_env = std::getenv("QDEC_CMP_LDS_PAD");
-            if (cap > 0 && !(pad_env && pad_env[0] == '0')) clds = std::max(clds, (size_t)(160 * 1024 / cap) / 16 * 16);
+            // padded to 1/cap of the CU
+            if (cap > 0) clds = std::max(clds, (size_t)(160 * 1024 / cap) / 16 * 16);
             // degree-3 rounds: the (2, 4, 7) shape instantiates D3R = 2 (n = 225 HGP: 144 degree-3 columns)
             if constexpr (RC == 2 && RV == 4 && DRC == 7) {
                 if (g.ms_d3r >= 2) {
@@ -913,8 +1146,15 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hip
             if (e2 != hipSuccess) return (int)e2;
             ss = a.ssf_stream;
         }
-        rc = g.n_gen <= 64 ? launch_ssf_wave<1, RV, RC>(g, a, num_cus, ss)
-                           : launch_ssf_wave<2, RV, RC>(g, a, num_cus, ss);
+        if (g.s_lut && g.opt_ssf == kSsfAuto) {
+            rc = g.n_gen <= 64 ? launch_ssf_lut<1, RV, RC>(g, a, num_cus, ss)
+                               : launch_ssf_lut<2, RV, RC>(g, a, num_cus, ss);
+        } else {
+            DevGraph gs = g;  // QD_SSF_SCAN_GATHER: no incremental local syndromes
+            if (g.opt_ssf == kSsfScanGather) gs.g_inv = nullptr;
+            rc = g.n_gen <= 64 ? launch_ssf_wave<1, RV, RC>(gs, a, num_cus, ss)
+                               : launch_ssf_wave<2, RV, RC>(gs, a, num_cus, ss);
+        }
         record_ev(a, 2, ss);
         return rc;
     }

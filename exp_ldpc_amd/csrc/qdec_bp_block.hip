@@ -1315,11 +1315,10 @@ static int launch_block2(K kern, size_t lds, int64_t work, int num_cus, hipStrea
 }
 
 // SSF + finalize of queued shots whose state fits LDS: the incremental kernel
-// when the inverse table exists (QDEC_SSF_INC=0 selects the re-scanning one).
+// when the inverse table exists (QD_OPT_SSF_INC = 0 selects the re-scanning one).
 static int launch_ssf_fin(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
-    const char* opt = getenv("QDEC_SSF_INC");
     const size_t lds = ssf_inc_lds(g);
-    if (a.ssf && g.g_iptr && g.n_gen <= 8192 && lds <= 160 * 1024 && !(opt && opt[0] == '0')) {
+    if (a.ssf && g.g_iptr && g.n_gen <= 8192 && lds <= 160 * 1024 && g.opt_ssf_inc) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ssf_inc_block_kernel),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
@@ -1377,10 +1376,9 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
         // message accesses of more resident shots only add HBM traffic: on C5 at
         // p = 0.005, 4 / 3 / 2 / 1 per CU ran 18.0 / 20.8 / 26.3 / 19.2 k shots/s
         // (scattered writes), 23.9 / 27.1 / 29.3 k (contiguous writes, vcsc), so
-        // placement 0 runs 2.  QDEC_BLOCK_WG_PER_CU overrides (diagnostic).
+        // placement 0 runs 2.  QD_OPT_BLOCK_WG overrides.
         if (placement == 0) cap = std::min(cap, 2);
-        if (const char* wv = getenv("QDEC_BLOCK_WG_PER_CU"))
-            if (atoi(wv) > 0) cap = std::min((int)(max_wg / num_cus), atoi(wv));
+        if (g.opt_block_wg > 0) cap = std::min((int)(max_wg / num_cus), g.opt_block_wg);
         a.work_ctr = static_cast<unsigned long long*>(scratch);
         gs = reinterpret_cast<T*>(static_cast<unsigned char*>(scratch) + kGrpHeader);
         const hipError_t e0 = hipMemsetAsync(a.work_ctr, 0, sizeof(unsigned long long), stream);
@@ -1416,7 +1414,7 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
 }
 
 // ---------------------------------------------------------------- LDS-resident launch
-// QDEC_LDS_KERNEL=0 disables bp_ms_lds_kernel, =1 forces it on any graph it can
+// QD_OPT_LDS_KERNEL = 0 disables bp_ms_lds_kernel, 1 forces it on any graph it can
 // hold (also those whose messages fit the small-graph LDS budget); by default
 // it takes the min-sum fp32 graphs whose messages would go to HBM.
 bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a) {
@@ -1424,9 +1422,8 @@ bool lds_kernel_applies(const DevGraph& g, int method, int precision, const Deco
     if (!a.syn || a.syn_flags || a.llr_out || !a.wave_ctr) return false;
     if (g.n > 16 * kMlThreads || g.m <= 0 || ml_lds_bytes(g) > 160 * 1024) return false;
     if (block_placement(g, 4) == 0) return false;  // the SSF/finalize state would not fit LDS
-    const char* opt = getenv("QDEC_LDS_KERNEL");
-    if (opt && opt[0] == '0') return false;
-    if (opt && opt[0] == '1') return true;
+    if (g.opt_lds_kernel == 0) return false;
+    if (g.opt_lds_kernel == 1) return true;
     return block_placement(g, 4) != 3;
 }
 
@@ -1468,11 +1465,11 @@ static int launch_lds(const DevGraph& g, const DecodeArgs& a, int num_cus, hipSt
 }
 
 // ---------------------------------------------------------------- slot-group launch
-// HBM budget of one handle's group scratch: QDEC_GROUP_SCRATCH_MB when set, else
+// HBM budget of one handle's group scratch: QD_OPT_GROUP_MB when set, else
 // a quarter of the device memory free right now (a bpssf_hybrid pipeline holds
 // two such handles; the batch cap in group_count keeps small decodes small)
-static size_t group_scratch_budget() {
-    if (const char* v = getenv("QDEC_GROUP_SCRATCH_MB")) return (size_t)std::max(64ll, atoll(v)) << 20;
+static size_t group_scratch_budget(const DevGraph& g) {
+    if (g.opt_group_mb > 0) return (size_t)std::max(64, g.opt_group_mb) << 20;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)4 << 30;
     return std::max<size_t>(free_b / 4, (size_t)64 << 20);
@@ -1512,23 +1509,22 @@ static int group_per_cu(const DevGraph& g, int method, size_t tsz) {
 static int64_t group_count(const DevGraph& g, int method, size_t tsz, int num_cus, int64_t B) {
     const size_t per = group_layout(g, tsz).total;
     int64_t c = std::min<int64_t>((int64_t)num_cus * group_per_cu(g, method, tsz),
-                                  (int64_t)(group_scratch_budget() / per));
+                                  (int64_t)(group_scratch_budget(g) / per));
     c = std::min<int64_t>(c, (B + 127) / 128);
     return std::max<int64_t>(c, 1);
 }
 
 // The slot-group kernel takes min-sum and product-sum graphs whose messages do
 // not fit the small-graph LDS budget (row degree <= 16, column degree <= 8, the
-// syndrome given directly).  QDEC_GROUP_KERNEL=0 disables it (workgroup kernel
+// syndrome given directly).  QD_OPT_GROUP_KERNEL = 0 disables it (workgroup kernel
 // with HBM message slices), =1 forces it on any graph within those degrees.
 // For fp32 min-sum graphs the LDS-resident kernel (bp_ms_lds_kernel) keeps
 // precedence unless the group kernel is forced.
 bool group_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a) {
     if (g.max_rdeg > 16 || g.max_cdeg > 8 || !a.syn || a.syn_flags) return false;
     (void)method;
-    const char* opt = getenv("QDEC_GROUP_KERNEL");
-    if (opt && opt[0] == '0') return false;
-    if (opt && opt[0] == '1') return true;
+    if (g.opt_group_kernel == 0) return false;
+    if (g.opt_group_kernel == 1) return true;
     return block_placement(g, precision == 1 ? 4 : 8) != 3;
 }
 
@@ -1589,9 +1585,7 @@ static int launch_group_shape(const DevGraph& g, const DecodeArgs& a, int num_cu
 
 size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num_cus, const DecodeArgs& a) {
     const size_t tsz = precision == 1 ? 4 : 8;
-    if (group_kernel_applies(g, method, precision, a) && !(lds_kernel_applies(g, method, precision, a) &&
-                                                           !(getenv("QDEC_GROUP_KERNEL") &&
-                                                             getenv("QDEC_GROUP_KERNEL")[0] == '1'))) {
+    if (group_kernel_applies(g, method, precision, a) && !(lds_kernel_applies(g, method, precision, a) && g.opt_group_kernel != 1)) {
         const size_t fin = (a.ssf && block_placement(g, tsz) == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g)
                                                                   : 0;
         return kGrpHeader + (size_t)group_count(g, method, tsz, num_cus, a.B) * group_layout(g, tsz).total + fin;
@@ -1612,9 +1606,7 @@ size_t block_scratch_floor(const DevGraph& g, int method, int precision, int num
     if (full == 0) return 0;
     const size_t tsz = precision == 1 ? 4 : 8;
     const size_t fin = (a.ssf && block_placement(g, tsz) == 0) ? (size_t)num_cus * kFinPerCu * block_state_stride(g) : 0;
-    if (group_kernel_applies(g, method, precision, a) && !(lds_kernel_applies(g, method, precision, a) &&
-                                                           !(getenv("QDEC_GROUP_KERNEL") &&
-                                                             getenv("QDEC_GROUP_KERNEL")[0] == '1')))
+    if (group_kernel_applies(g, method, precision, a) && !(lds_kernel_applies(g, method, precision, a) && g.opt_group_kernel != 1))
         return std::min(full, kGrpHeader + group_layout(g, tsz).total + fin);
     return full;  // workgroup slices: the launch needs its per-CU slices
 }
@@ -1623,9 +1615,8 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
                         hipStream_t stream, void* scratch, size_t scratch_bytes) {
     if (a.B <= 0) return 0;
     if (a.ssf && g.n_gen <= 0) return (int)hipErrorInvalidValue;
-    const char* gopt = getenv("QDEC_GROUP_KERNEL");
     const bool lds = lds_kernel_applies(g, method, precision, a);
-    if (group_kernel_applies(g, method, precision, a) && !(lds && !(gopt && gopt[0] == '1'))) {
+    if (group_kernel_applies(g, method, precision, a) && !(lds && g.opt_group_kernel != 1)) {
         if (precision == 1)
             return method == 1 ? launch_group_shape<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                                : launch_group_shape<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);

@@ -16,6 +16,8 @@ constexpr int kMlDC = 4;         // LDS-resident min-sum kernel: max variable de
 constexpr int kGenW = 8;         // max flip-set generator weight (255 subsets)
 constexpr int kGenLC = 32;       // max local checks per generator (u32 masks)
 constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F|)
+constexpr int kLutLC = 16;       // table-driven SSF: max local checks per generator (16-bit local syndromes)
+constexpr int kLutLCW = kLutLC / 4;  // words of u8 local-check ids per generator
 constexpr int kEdgePad = 16;     // index / prior arrays padded past E (>= the largest row / column width)
 constexpr int kCmpSegs = 64;     // segments (and counters) of the compact shot list
 // entries a compact-list segment must hold for a batch of B shots (64-shot tiles)
@@ -123,6 +125,22 @@ struct DevGraph {
     // (ssf_inc_block_kernel; nullptr when n_gen >= 65536)
     const int32_t* g_iptr;
     const uint32_t* g_ient;
+    // table-driven SSF (ssf_lut_kernel, qdec_bp.hip; built by ssf_lut_tables in
+    // qdec_abi.cpp, nullptr when the graph does not qualify).  A generator's
+    // local checks are put in a canonical order (by the set of its qubits that
+    // touch them), so generators with the same local structure share one table
+    // over their <= 16-bit local syndrome sl: s_lut[s_off[g] + sl] = rank << 24 |
+    // M_t << 8 | t, t the spec's best subset (lowest bitmask among the best
+    // gain/|t|), M_t the local checks it toggles, rank the position of its score
+    // among all positive scores (0: no positive gain).  s_lcw: the canonical local
+    // checks as u8 ids, 4 per word ([kLutLCW][g_pad], pad 0xff); s_tog: per check
+    // c and lane l the local-syndrome bits that toggle when c flips, generator l
+    // in the low half-word, generator 64 + l in the high one ([m_pad][64]).
+    const uint32_t* s_lut;
+    int s_lut_n;
+    const uint32_t* s_off;
+    const uint32_t* s_lcw;
+    const uint32_t* s_tog;
     // logicals (fused failure check)
     int k, lz_words;
     const uint64_t* lz;           // [k][lz_words]    bit q%64 of word q/64 (nullptr when too large)
@@ -133,7 +151,31 @@ struct DevGraph {
     const int32_t* lz_ptr;        // [k+1]
     const int32_t* lz_idx;        // [nnz]
     int lz_sparse;
+    // per-handle kernel choices (qd_graph_set_option, QD_OPT_* in include/qdec.h;
+    // defaults from default_options): the launchers read these, never the
+    // environment
+    int opt_compact;       // 1: two-pass lean min-sum decodes (triage + compact list); 0: one-pass kernel
+    int opt_triage_it1;    // 1: min-sum iteration 1 inside the triage; 0: left to the BP kernel
+    int opt_ssf;           // QD_SSF_*: table-driven, scanning (incremental / re-gathered / unsplit scorer)
+    int opt_lds_kernel;    // -1: automatic; 0: never; 1: forced (bp_ms_lds_kernel)
+    int opt_group_kernel;  // -1: automatic; 0: never; 1: forced (bp_group_kernel)
+    int opt_ssf_inc;       // 1: incremental workgroup SSF (ssf_inc_block_kernel); 0: the re-scanning one
+    int opt_block_wg;      // > 0: workgroups per CU of the HBM-slice workgroup kernels (0: automatic)
+    int opt_group_mb;      // > 0: HBM budget of the slot-group scratch in MiB (0: a quarter of free HBM)
 };
+
+// SSF kernel choice of wave graphs (DevGraph::opt_ssf)
+enum { kSsfAuto = 0, kSsfScan = 1, kSsfScanGather = 2, kSsfScanNoSplit = 3 };
+inline void default_options(DevGraph& g) {
+    g.opt_compact = 1;
+    g.opt_triage_it1 = 1;
+    g.opt_ssf = kSsfAuto;
+    g.opt_lds_kernel = -1;
+    g.opt_group_kernel = -1;
+    g.opt_ssf_inc = 1;
+    g.opt_block_wg = 0;
+    g.opt_group_mb = 0;
+}
 
 struct DecodeArgs {
     int64_t B;

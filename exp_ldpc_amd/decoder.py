@@ -22,7 +22,17 @@ import scipy.sparse as sp
 
 from . import _abi
 
-__all__ = ["Decoder", "parse_bp_method", "as_csr01"]
+__all__ = ["Decoder", "parse_bp_method", "as_csr01", "OPTIONS", "DEFAULT_OPTIONS"]
+
+# per-handle kernel choices (qd_graph_set_option, QD_OPT_* in include/qdec.h);
+# every choice gives identical results, they exist for A/B measurements and so
+# tests keep each kernel path covered
+OPTIONS = {"compact": 1, "triage_it1": 2, "ssf": 3, "lds_kernel": 4, "group_kernel": 5, "ssf_inc": 6,
+           "block_wg": 7, "group_mb": 8}
+SSF_KERNELS = {"auto": 0, "scan": 1, "scan_gather": 2, "scan_nosplit": 3}  # values of the "ssf" option
+# options applied to every Decoder built afterwards (tests patch this dict to
+# route pipelines that build their decoders internally through one kernel path)
+DEFAULT_OPTIONS: dict = {}
 
 _PS_NAMES = {"ps", "product_sum", "prod_sum", "0", "prod sum", "product sum"}
 _MS_NAMES = {"ms", "minimum_sum", "min_sum", "1", "minimum sum", "min sum",
@@ -84,6 +94,8 @@ class Decoder:
         _abi.check(self._lib.qd_graph_create(self.m, self.n, _abi.ptr(rp), _abi.ptr(ci), self.n_data,
                                              self.fold_blocks, self.device, C.byref(self._handle)),
                    "qd_graph_create")
+        for name, value in DEFAULT_OPTIONS.items():
+            self.set_option(name, value)
         self.method = parse_bp_method(method)
         self.precision = parse_precision(precision)
         self.max_iter = int(max_iter)
@@ -257,6 +269,24 @@ class Decoder:
         streams.  Results do not depend on it."""
         _abi.check(self._lib.qd_graph_set_wave_occupancy(self._handle, int(waves_per_cu)),
                    "qd_graph_set_wave_occupancy")
+
+    def set_option(self, name: str, value) -> None:
+        """Kernel choice of this handle (qd_graph_set_option): name in OPTIONS;
+        for "ssf" the value may be a SSF_KERNELS name."""
+        if name == "ssf" and isinstance(value, str):
+            value = SSF_KERNELS[value]
+        _abi.check(self._lib.qd_graph_set_option(self._handle, OPTIONS[name], int(value)), f"set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int32(0)
+        _abi.check(self._lib.qd_graph_get_option(self._handle, OPTIONS[name], C.byref(v)), f"get_option({name})")
+        return v.value
+
+    def ssf_tables(self) -> tuple[bool, int]:
+        """(the graph qualifies for the table-driven SSF kernel, its table bytes)."""
+        has, nb = C.c_int32(0), C.c_int64(0)
+        _abi.check(self._lib.qd_graph_ssf_tables(self._handle, C.byref(has), C.byref(nb)), "qd_graph_ssf_tables")
+        return bool(has.value), int(nb.value)
 
     def set_ssf_stream(self, stream) -> None:
         """Run the SSF kernel of later decode_device calls on `stream` (a torch

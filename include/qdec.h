@@ -211,6 +211,58 @@ int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_c
 int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int32_t ssf_len, char* pre,
                           int32_t pre_len);
 
+/* Kernel choices of one handle, for A/B measurements and for tests that keep
+ * every kernel path covered.  Results are identical under every setting (each
+ * path is parity-tested against the oracle).  Returns -2 for an unknown option
+ * or an out-of-range value.  No reference counterpart: ldpc has one decoder
+ * implementation.
+ *   QD_OPT_COMPACT       1 (default): lean min-sum decodes on wave graphs run the
+ *                        shot triage + compact-list kernel; 0: the one-pass kernel.
+ *   QD_OPT_TRIAGE_IT1    1 (default): the triage runs min-sum iteration 1
+ *                        bit-sliced (default alpha schedule, positive priors); 0: off.
+ *   QD_OPT_SSF           SSF kernel of wave graphs: QD_SSF_AUTO (default: the
+ *                        table-driven kernel when the graph's tables qualify, else
+ *                        the scanning kernel), QD_SSF_SCAN (scanning kernel,
+ *                        incremental local syndromes), QD_SSF_SCAN_GATHER (scanning
+ *                        kernel, local syndromes re-gathered every step),
+ *                        QD_SSF_SCAN_NOSPLIT (scanning, one lane per generator).
+ *   QD_OPT_LDS_KERNEL    -1 (default) automatic, 0 never, 1 forced: the
+ *                        LDS-resident f32 min-sum workgroup kernel.
+ *   QD_OPT_GROUP_KERNEL  -1 (default) automatic, 0 never, 1 forced: the slot-group
+ *                        HBM-streaming kernel.
+ *   QD_OPT_SSF_INC       1 (default): incremental workgroup SSF; 0: re-scanning.
+ *   QD_OPT_BLOCK_WG      0 (default) automatic, N > 0: workgroups per CU of the
+ *                        HBM-slice workgroup BP kernel.
+ *   QD_OPT_GROUP_MB      0 (default): a quarter of the free HBM, N > 0: N MiB for
+ *                        the slot-group kernel's message scratch. */
+#define QD_OPT_COMPACT 1
+#define QD_OPT_TRIAGE_IT1 2
+#define QD_OPT_SSF 3
+#define QD_OPT_LDS_KERNEL 4
+#define QD_OPT_GROUP_KERNEL 5
+#define QD_OPT_SSF_INC 6
+#define QD_OPT_BLOCK_WG 7
+#define QD_OPT_GROUP_MB 8
+#define QD_SSF_AUTO 0
+#define QD_SSF_SCAN 1
+#define QD_SSF_SCAN_GATHER 2
+#define QD_SSF_SCAN_NOSPLIT 3
+int qd_graph_set_option(qd_graph* g, int32_t option, int32_t value);
+int qd_graph_get_option(const qd_graph* g, int32_t option, int32_t* value);
+
+/* Which SSF kernel the handle's graph qualifies for on its own: 1 when the
+ * table-driven kernel's tables were built (QD_SSF_AUTO then runs it), 0
+ * otherwise.  *lut_bytes (nullable) = bytes of its score tables.  No reference
+ * counterpart. */
+int qd_graph_ssf_tables(const qd_graph* g, int32_t* has_lut, int64_t* lut_bytes);
+/* Copies of the table-driven SSF kernel's tables, for host-only graphs
+ * (qd_graph_create_host; tests emulate the kernel's steps on them): lut
+ * [lut_bytes / 4], off [g_pad], lcw [4][g_pad], tog [m_pad][64] (u32 each; the
+ * layouts of DevGraph::s_lut / s_off / s_lcw / s_tog in qdec_internal.h);
+ * *g_pad and *m_pad receive the strides.  Any output may be NULL. */
+int qd_graph_ssf_tables_copy(const qd_graph* g, uint32_t* lut, uint32_t* off, uint32_t* lcw, uint32_t* tog,
+                             int32_t* g_pad, int32_t* m_pad);
+
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */
 int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream);

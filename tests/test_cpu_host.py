@@ -314,3 +314,103 @@ def test_host_only_tables_build_without_a_gpu(code225):
         lib.qd_graph_destroy(h)
     for h in (h1, h2, h3):
         assert lib.qd_graph_destroy(h) == 0
+
+
+def _lut_ssf_emulate(tab, H, gens, x, resid, max_steps=0):
+    """The table-driven SSF kernel's steps (ssf_lut_kernel, qdec_bp.hip) run on
+    the host over the library's own tables: local syndromes from the toggle rows
+    of the violated checks, then per step the table entry of every generator,
+    the max of (rank, -g), the winner's subset applied (qubits x, toggle rows of
+    the checks it flips).  Returns (x, steps)."""
+    lut, off, lcw, tog, gp = tab
+    x = x.copy()
+    ng = gens.shape[0]
+    gq = [gens.indices[gens.indptr[g]:gens.indptr[g + 1]] for g in range(ng)]
+    sl = np.zeros(ng, np.int64)
+    for c in np.flatnonzero(resid):
+        for g in range(ng):
+            sl[g] ^= (int(tog[c, g & 63]) >> (16 * (g >> 6))) & 0xffff
+    sw = int(resid.sum())
+    steps = 0
+    while sw > 0 and (max_steps <= 0 or steps < max_steps):
+        best, bg = 0, -1
+        for g in range(ng):
+            e = int(lut[off[g] + sl[g]])
+            if e >> 24:
+                key = ((e >> 24) << 15) | ((127 - g) << 8) | (e & 0xff)
+                if key > best:
+                    best, bg = key, g
+        if bg < 0:
+            break
+        e = int(lut[off[bg] + sl[bg]])
+        t, fm = e & 0xff, (e >> 8) & 0xffff
+        slg = int(sl[bg])
+        sw -= bin(slg).count("1") - bin(slg ^ fm).count("1")
+        steps += 1
+        for b in range(16):
+            if (fm >> b) & 1:
+                c = (int(lcw[b // 4, bg]) >> (8 * (b % 4))) & 0xff
+                for g in range(ng):
+                    sl[g] ^= (int(tog[c, g & 63]) >> (16 * (g >> 6))) & 0xffff
+        for k in range(len(gq[bg])):
+            if (t >> k) & 1:
+                x[gq[bg][k]] ^= 1
+    return x, steps
+
+
+def _lut_tables(lib, h):
+    import ctypes as C
+
+    from exp_ldpc_amd import _abi
+    has, nb = C.c_int32(0), C.c_int64(0)
+    _abi.check(lib.qd_graph_ssf_tables(h, C.byref(has), C.byref(nb)), "ssf_tables")
+    if not has.value:
+        return None
+    gp, mp = C.c_int32(0), C.c_int32(0)
+    _abi.check(lib.qd_graph_ssf_tables_copy(h, None, None, None, None, C.byref(gp), C.byref(mp)), "copy")
+    lut = np.zeros(nb.value // 4, np.uint32)
+    off = np.zeros(gp.value, np.uint32)
+    lcw = np.zeros((4, gp.value), np.uint32)
+    tog = np.zeros((mp.value, 64), np.uint32)
+    _abi.check(lib.qd_graph_ssf_tables_copy(h, _abi.ptr(lut), _abi.ptr(off), _abi.ptr(lcw), _abi.ptr(tog), None,
+                                            None), "copy")
+    return lut, off, lcw, tog, gp.value
+
+
+@pytest.mark.parametrize("max_steps", [0, 2])
+def test_ssf_lut_tables_follow_the_spec(code225, oracle_lib, max_steps):
+    """The table-driven SSF kernel's tables (ssf_lut_tables, qdec_abi.cpp) on the
+    n = 225 HGP code: every generator shares ONE 4096-entry score table (same
+    4 x 3 local pattern after the canonical local-check order), and the kernel's
+    step rule run on the host over those exact tables reproduces the oracle's
+    SSF (oracle/qdec_oracle.c ssf_run_fast: x and step counts) on BP-failed
+    shots."""
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    hz, hx, lz = code225.checks.z, code225.checks.x, code225.logicals.z
+    h, _, _ = _host_graph(lib, hz, gens=hx, lz=lz, probs=0.02)
+    try:
+        tab = _lut_tables(lib, h)
+        assert tab is not None
+        lut, off = tab[0], tab[1]
+        assert lut.size == 4096 and not off[:hx.shape[0]].any()
+        ranks = sorted({int(e) >> 24 for e in lut} - {0})
+        assert ranks == list(range(1, len(ranks) + 1))
+        rng = np.random.default_rng(11)
+        B = 160
+        err = (rng.random((B, hz.shape[1])) < 0.06).astype(np.uint8)
+        syn = ((hz @ err.T).T % 2).astype(np.uint8)
+        hx = sp.csr_matrix(hx)
+        hx.sort_indices()
+        bp = oracle_lib.decode(hz, 0.02, syn, method="ms", precision="f64", max_iter=1, ssf=False, want_llr=False)
+        ref = oracle_lib.decode(hz, 0.02, syn, method="ms", precision="f64", max_iter=1, ssf=True, gens=hx,
+                                ssf_max_steps=max_steps, want_llr=False)
+        checked = 0
+        for b in np.flatnonzero((bp["status"] & 1) == 0):
+            resid = (syn[b] ^ (hz @ bp["x"][b]) % 2).astype(np.uint8)
+            x, steps = _lut_ssf_emulate(tab, hz, hx, bp["x"][b], resid, max_steps)
+            assert np.array_equal(x, ref["x"][b]) and steps == ref["ssf_steps"][b], b
+            checked += 1
+        assert checked > 100 and ref["ssf_steps"].sum() > 200
+    finally:
+        lib.qd_graph_destroy(h)

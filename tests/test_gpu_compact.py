@@ -5,7 +5,7 @@ tile and the 4-entry chunks, syndrome / readout buffers whose byte length is
 not a multiple of 4, more than 64 logicals (several readout-parity words),
 no fused check, partial outputs, zero-syndrome shots with and without positive
 priors, and the SSF queue carrying readout parities.  Every output equals the
-oracle's; the one-pass kernel (QDEC_COMPACT=0) gives the same bytes."""
+oracle's; the one-pass kernel (QD_OPT_COMPACT = 0) gives the same bytes."""
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -65,16 +65,16 @@ def test_compact_every_wave_shape(gpu_available, oracle_lib, precision, mn, monk
                                     want_llr=False)
             for key in got:
                 assert np.array_equal(got[key], ref[key]), (k, B, key)
-            monkeypatch.setenv("QDEC_COMPACT", "0")
+            dec.set_option("compact", 0)
             one, (bp1, _, _) = _decode_device(dec, syn, rd)
-            monkeypatch.delenv("QDEC_COMPACT")
+            dec.set_option("compact", 1)
             assert "bp_ms_wave_kernel" in bp1
             for key in got:
                 assert np.array_equal(one[key], got[key]), (k, B, key)
             # iteration 1 left to the BP kernel (the triage only lists)
-            monkeypatch.setenv("QDEC_TRIAGE_IT1", "0")
+            dec.set_option("triage_it1", 0)
             lst, _ = _decode_device(dec, syn, rd)
-            monkeypatch.delenv("QDEC_TRIAGE_IT1")
+            dec.set_option("triage_it1", 1)
             for key in got:
                 assert np.array_equal(lst[key], got[key]), (k, B, key)
 
@@ -139,10 +139,12 @@ def test_compact_ssf_rpar_and_partial_outputs(gpu_available, oracle_lib, precisi
         ref = oracle_lib.decode(hz, 0.027, syn, method="ms", precision=precision, max_iter=30, ssf=True, gens=hx, lz=L,
                                 readout=rd, want_llr=False, ssf_impl="fast")
         assert ref["ssf_steps"].sum() > 0 and ref["fail"].any()
-        got, (bp_k, ssf_k, _) = _decode_device(dec, syn, rd)
-        assert "cmp_kernel" in bp_k and "ssf_wave_kernel" in ssf_k
-        for key in got:
-            assert np.array_equal(got[key], ref[key]), (extra, key)
+        for kern, name in (("scan", "ssf_wave_kernel"), ("auto", "ssf_lut_kernel")):
+            dec.set_option("ssf", kern)
+            got, (bp_k, ssf_k, _) = _decode_device(dec, syn, rd)
+            assert "cmp_kernel" in bp_k and name in ssf_k, (bp_k, ssf_k)
+            for key in got:
+                assert np.array_equal(got[key], ref[key]), (extra, kern, key)
         part, _ = _decode_device(dec, syn, rd, keys=("fail",))
         assert np.array_equal(part["fail"], ref["fail"])
         part, _ = _decode_device(dec, syn, rd, keys=("iters", "status"))

@@ -19,6 +19,8 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
+from exp_ldpc_amd import decoder
+
 from conftest import load_checks
 
 pytestmark = pytest.mark.gpu
@@ -87,9 +89,9 @@ def test_hgp10k_bp_ssf_parity(gpu_available, oracle_lib, hgp10k):
 
 
 def test_hgp10k_group_kernel_forced_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
-    """The slot-group HBM-streaming kernel forced (QDEC_GROUP_KERNEL=1) on C4 in
+    """The slot-group HBM-streaming kernel forced (QD_OPT_GROUP_KERNEL = 1) on C4 in
     fp32, where the LDS-resident kernel is the default."""
-    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1")
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "group_kernel", 1)
     hx, hz, lz = hgp10k
     p = 0.03
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=9, shot0=0, B=160)
@@ -157,7 +159,7 @@ def test_psl13_lift_spacetime_r1_parity(gpu_available, oracle_lib, psl13_hz, ker
     storage-experiment sampler at R = 1 and folded onto the data qubits; both
     HBM-message kernels."""
     from exp_ldpc_amd.spacetime import SpacetimeCode
-    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1" if kernel == "group" else "0")
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "group_kernel", 1 if kernel == "group" else 0)
     hz = psl13_hz
     H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
     p = 0.005
@@ -193,10 +195,10 @@ def test_hgp10k_lds_kernel_parity(gpu_available, oracle_lib, hgp10k, p):
 
 
 def test_hgp10k_workgroup_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
-    """The HBM-message workgroup kernel stays covered on C4 (QDEC_LDS_KERNEL=0,
-    QDEC_GROUP_KERNEL=0)."""
-    monkeypatch.setenv("QDEC_LDS_KERNEL", "0")
-    monkeypatch.setenv("QDEC_GROUP_KERNEL", "0")
+    """The HBM-message workgroup kernel stays covered on C4 (QD_OPT_LDS_KERNEL = 0,
+    QD_OPT_GROUP_KERNEL = 0)."""
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 0)
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "group_kernel", 0)
     hx, hz, lz = hgp10k
     p = 0.03
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=12, shot0=0, B=96)
@@ -205,11 +207,11 @@ def test_hgp10k_workgroup_kernel_parity(gpu_available, oracle_lib, hgp10k, monke
 
 @pytest.mark.parametrize("seed", [3, 4])
 def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatch):
-    """bp_ms_lds_kernel forced (QDEC_LDS_KERNEL=1) on ragged graphs outside the wave
+    """bp_ms_lds_kernel forced (QD_OPT_LDS_KERNEL = 1) on ragged graphs outside the wave
     shapes: check degrees 0..8 (empty and single-edge rows), variable degrees
     0..4, per-column priors, ms_scaling both ways; x / iterations / status."""
     from exp_ldpc_amd.codes import make_check_matrix
-    monkeypatch.setenv("QDEC_LDS_KERNEL", "1")
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
     rng = np.random.default_rng(seed)
     m, n = int(rng.integers(600, 1500)), int(rng.integers(700, 3000))
     rows, colcount = [], np.zeros(n, int)
@@ -228,9 +230,9 @@ def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatc
 
 
 def test_hgp10k_ssf_rescan_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
-    """The re-scanning SSF block kernel (QDEC_SSF_INC=0) stays covered; the
+    """The re-scanning SSF block kernel (QD_OPT_SSF_INC = 0) stays covered; the
     default incremental one is covered by every other C4 test."""
-    monkeypatch.setenv("QDEC_SSF_INC", "0")
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "ssf_inc", 0)
     hx, hz, lz = hgp10k
     p = 0.03
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=13, shot0=0, B=96)
@@ -255,7 +257,7 @@ def c5():
 def test_c5_r0_bp_ssf_fail_parity(gpu_available, oracle_lib, c5, precision, kernel, monkeypatch):
     """Config 5 at R = 0: BP min-sum (max_iter 50) + SSF on the Hx flip sets +
     logical check, 256 sampled shots, every output bit-exact."""
-    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1" if kernel == "group" else "0")
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "group_kernel", 1 if kernel == "group" else 0)
     hx, hz, lz = c5
     p = 0.004
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=21, shot0=0, B=256)
@@ -301,7 +303,7 @@ def test_group_kernel_llr_and_ragged(gpu_available, oracle_lib, monkeypatch):
     from test_gpu_parity import _cmp_llr
     from exp_ldpc_amd.codes import make_check_matrix
     from exp_ldpc_amd.decoder import Decoder
-    monkeypatch.setenv("QDEC_GROUP_KERNEL", "1")
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "group_kernel", 1)
     rng = np.random.default_rng(17)
     m, n = 700, 1500
     rows, colcount = [], np.zeros(n, int)

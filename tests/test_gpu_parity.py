@@ -62,25 +62,24 @@ def test_bp_parity(gpu_available, oracle_lib, method, precision, shape):
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("max_iter", [1, 3, 50])
-@pytest.mark.parametrize("local_syndromes", ["incremental", "gather", "nosplit"])
-def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, local_syndromes, code225, monkeypatch):
-    """Both ways the wave SSF kernel keeps generator-local syndromes: updated
-    through the check -> generator table after each flip (default), or
-    re-gathered from the residual every step (QDEC_SSF_GATHER=1); and with the
-    two-lanes-per-generator scoring of short listing steps off
-    (QDEC_SSF_NOSPLIT=1)."""
+@pytest.mark.parametrize("ssf_kernel", ["auto", "scan", "scan_gather", "scan_nosplit"])
+def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, ssf_kernel, code225):
+    """Every wave SSF kernel against the oracle: the table-driven kernel (the
+    default on this code: one score table for all 108 generators), and the
+    scanning kernel with its local syndromes updated through the check ->
+    generator table after each flip, re-gathered from the residual every step,
+    or scored one lane per generator (QD_OPT_SSF)."""
     from exp_ldpc_amd.decoder import Decoder
-    if local_syndromes == "gather":
-        monkeypatch.setenv("QDEC_SSF_GATHER", "1")
-    if local_syndromes == "nosplit":
-        monkeypatch.setenv("QDEC_SSF_NOSPLIT", "1")
     rng = np.random.default_rng(max_iter)
     B = 2000
     rd = _errors(rng, B, 225, 0.03)
     syn = ((HZ @ rd.T).T % 2).astype(np.uint8)
     lz = code225.logicals.z
     dec = Decoder(HZ, 0.02, method="ms", precision=precision, max_iter=max_iter, flip_sets=HX, logicals=lz)
+    dec.set_option("ssf", ssf_kernel)
+    assert dec.ssf_tables()[0]
     got = dec.decode(syn, readout=rd, want=("x", "corr", "iters", "status", "ssf_steps", "fail"))
+    assert ("ssf_lut_kernel" if ssf_kernel == "auto" else "ssf_wave_kernel") in dec.last_kernels()[1]
     ref = oracle_lib.decode(HZ, 0.02, syn, method="ms", precision=precision, max_iter=max_iter, ssf=True, gens=HX,
                             lz=lz, readout=rd, want_llr=False)
     for key in ("x", "corr", "iters", "status", "ssf_steps", "fail"):
@@ -89,7 +88,8 @@ def test_bp_ssf_parity(gpu_available, oracle_lib, precision, max_iter, local_syn
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
-def test_bp_ssf_parity_long_queue(gpu_available, oracle_lib, precision, code225):
+@pytest.mark.parametrize("ssf_kernel", ["auto", "scan"])
+def test_bp_ssf_parity_long_queue(gpu_available, oracle_lib, precision, ssf_kernel, code225):
     """A queue long enough (2^18 BP failures, >= 16 slots per SSF wave) that the
     SSF kernel hands out its tail from the slot counter; shots are independent,
     so a random subset decoded by the oracle checks every output bit-exactly."""
@@ -100,7 +100,9 @@ def test_bp_ssf_parity_long_queue(gpu_available, oracle_lib, precision, code225)
     syn = ((HZ @ rd.T).T % 2).astype(np.uint8)
     lz = code225.logicals.z
     dec = Decoder(HZ, 0.05, method="ms", precision=precision, max_iter=2, flip_sets=HX, logicals=lz)
+    dec.set_option("ssf", ssf_kernel)
     got = dec.decode(syn, readout=rd, want=("x", "corr", "iters", "status", "ssf_steps", "fail"))
+    assert ("ssf_lut_kernel" if ssf_kernel == "auto" else "ssf_wave_kernel") in dec.last_kernels()[1]
     assert (got["status"] & 1).mean() < 0.05  # nearly every shot went to the SSF queue
     idx = np.sort(rng.choice(B, 3000, replace=False))  # ~600 of them from counter-handed slots
     ref = oracle_lib.decode(HZ, 0.05, syn[idx], method="ms", precision=precision, max_iter=2, ssf=True, gens=HX,
@@ -374,10 +376,11 @@ def test_empty_batch_and_buffer_validation(gpu_available):
 
 @pytest.mark.parametrize("name", BLOCK_GRAPHS)
 def test_lds_kernel_block_graphs(gpu_available, oracle_lib, name, monkeypatch):
-    """bp_ms_lds_kernel forced (QDEC_LDS_KERNEL=1) on the workgroup-kernel graphs,
+    """bp_ms_lds_kernel forced (QD_OPT_LDS_KERNEL = 1) on the workgroup-kernel graphs,
     min-sum f32 (its only configuration): x / iterations / status bit-exact."""
     from exp_ldpc_amd.decoder import Decoder
-    monkeypatch.setenv("QDEC_LDS_KERNEL", "1")
+    from exp_ldpc_amd import decoder
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
     H, _ = _graph(name)
     H = sp.csr_matrix(H)
     rng = np.random.default_rng(len(name) + 1)
@@ -397,7 +400,8 @@ def test_lds_kernel_ssf_fold(gpu_available, oracle_lib, code225, monkeypatch):
     onto the data qubits (fold_blocks = 3) and the fused logical check."""
     from conftest import load_code
     from exp_ldpc_amd.decoder import Decoder
-    monkeypatch.setenv("QDEC_LDS_KERNEL", "1")
+    from exp_ldpc_amd import decoder
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
     code = load_code("hgp_36_3_4_s42_g4")
     hx, hz = code.checks.x, code.checks.z
     rng = np.random.default_rng(9)
@@ -425,12 +429,11 @@ def test_lds_kernel_ssf_fold(gpu_available, oracle_lib, code225, monkeypatch):
 @pytest.fixture(params=["compact", "onepass"])
 def lean_path(request, monkeypatch):
     """Lean launches run the two-pass compact path (ms_triage_kernel +
-    bp_ms_cmp_kernel) by default; QDEC_COMPACT=0 keeps the one-pass
+    bp_ms_cmp_kernel) by default; QD_OPT_COMPACT = 0 keeps the one-pass
     bp_ms_wave_kernel.  Lean tests run both."""
+    from exp_ldpc_amd import decoder
     if request.param == "onepass":
-        monkeypatch.setenv("QDEC_COMPACT", "0")
-    else:
-        monkeypatch.delenv("QDEC_COMPACT", raising=False)
+        monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "compact", 0)
     return request.param
 
 
