@@ -71,7 +71,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from exp_ldpc_amd.sharding import barrier, max_time, reduce_counts  # noqa: E402  (pure Python, no GPU)
+from exp_ldpc_amd.sharding import barrier, gather_rows, max_time, reduce_counts  # noqa: E402  (pure Python, no GPU)
 
 METRIC = "decoded syndrome shots/sec + logical error rate, (3,4)-HGP n=225 @ 1/2/4/8 GPUs"
 CODE = "hgp_12_3_4_s1234"
@@ -79,6 +79,7 @@ SEED = 20250221
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b64/b128 rate, every CU streaming (MI355X_MICROARCH.md §LDS)
 IO_BYTES_PER_SHOT = 108 + 225 + 1 + 1 + 4  # syndrome + readout in; fail, status, iters out
+TRIAGE_BYTES_PER_SHOT = 108 + 225  # the triage reads each shot's syndrome and readout rows
 
 
 def wilson(k: int, n: int, z: float = 1.96):
@@ -122,43 +123,63 @@ def pmc_ceilings(kernel: str):
     return None
 
 
-def lds_roofline(bp_ms, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms):
+def lds_roofline(bp_ms, pre_ms, listed, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms):
     """Roofline of the dominant kernel, the BP kernel at n = 225: its messages
     never leave the CU, so the unit that bounds it is the LDS.  achieved =
     algorithmic LDS bytes of the isolated launches (per shot-iteration: every
     edge's v2c message read by its check (8 B) and written back by its variable
     (8 B), every edge's (m1, m2) check state gathered by its variable (16 B),
-    every check's state written (16 B); counted from the launches' own
-    iteration totals) / their HIP-event durations; peak = the LDS's aggregate
-    rate with every CU streaming (MI355X_MICROARCH.md §LDS: ~150 TB/s for
-    ds_read_b64/b128).  The HBM line (compulsory I/O per shot) is kept beside
-    it, per launch and per sweep point."""
+    every check's state written (16 B)) / the BP kernel's own HIP-event
+    duration.  Only the shots the BP kernel decoded count: on the two-pass path
+    the triage finishes zero-syndrome and iteration-1-converged shots itself
+    (they report 1 iteration and never touch the BP kernel's LDS), so a launch's
+    iterations are sum(iters) - (B - listed), listed = the triage's compact-list
+    length; the triage's own time (HBM-streaming, `triage`) is kept out of the
+    BP kernel's and reported beside it.  peak = the LDS's aggregate rate with
+    every CU streaming (MI355X_MICROARCH.md §LDS: ~150 TB/s for
+    ds_read_b64/b128).  The HBM line (compulsory I/O per shot) is kept beside it,
+    per launch and per sweep point."""
     E, m = int(hz.nnz), int(hz.shape[0])
     lds_per_it = 32 * E + 16 * m
+    B = args.batch
+    it_bp = np.where(listed >= 0, it_iso - (B - listed), it_iso).astype(np.float64)
+    stage_ms = bp_ms + pre_ms
     tot_ms = float(bp_ms.sum())
-    lds_bytes = float(lds_per_it * it_iso.sum())
+    lds_bytes = float(lds_per_it * it_bp.sum())
     achieved = lds_bytes / (tot_ms * 1e-3) / 1e9
-    io_launch = IO_BYTES_PER_SHOT * args.batch
-    hbm_ach = io_launch / (bp_ms.mean() * 1e-3) / 1e9
+    io_launch = IO_BYTES_PER_SHOT * B
+    hbm_ach = io_launch / (stage_ms.mean() * 1e-3) / 1e9
+    tri_bytes = TRIAGE_BYTES_PER_SHOT * B
     per_point = {}
     for pi in range(bp_ms.shape[1]):
         ms = float(bp_ms[:, pi].mean())
-        per_point[str(pi)] = {"bp_ms": ms, "hbm_frac": io_launch / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                              "lds_frac": lds_per_it * float(it_iso[:, pi].mean()) / (ms * 1e-3) / 1e9 / LDS_PEAK_GBS}
+        st = float(stage_ms[:, pi].mean())
+        tr = float(pre_ms[:, pi].mean())
+        per_point[str(pi)] = {"bp_ms": ms, "triage_ms": tr, "bp_stage_ms": st,
+                              "listed_frac": float(listed[:, pi].mean() / B) if (listed[:, pi] >= 0).all() else None,
+                              "hbm_frac": io_launch / (st * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "lds_frac": lds_per_it * float(it_bp[:, pi].mean()) / (ms * 1e-3) / 1e9 / LDS_PEAK_GBS,
+                              "triage_hbm_frac": tri_bytes / (tr * 1e-3) / 1e9 / HBM_PEAK_GBS if tr > 0 else None}
     return {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": achieved / LDS_PEAK_GBS,
             "traffic": None, "kernel": bp_kernel, "avg_launch_ms": float(bp_ms.mean()), "launches": int(bp_ms.size),
-            "timing": "HIP events recorded by the library on the launch stream around each kernel, isolated phase "
-                      "(one stream)",
+            "timing": "HIP events recorded by the library on the launch stream around the BP kernel alone (the "
+                      "triage pass before it has its own event pair), isolated phase (one stream)",
             "algorithmic_bytes_per_launch": lds_bytes / bp_ms.size,
             "bytes_model": f"LDS: 32 B per edge + 16 B per check per BP iteration ({lds_per_it} B per shot-iteration "
-                           f"at E={E}, m={m}) x the launch's summed iterations",
+                           f"at E={E}, m={m}) x the iterations of the shots the BP kernel decoded "
+                           "(sum(iters) - (B - listed))",
             "hbm": {"achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": io_launch,
                     "bytes_model": f"per shot {IO_BYTES_PER_SHOT} B compulsory HBM I/O (108 B syndrome + 225 B "
-                                   "readout in, fail + status + int32 iterations out)"},
+                                   "readout in, fail + status + int32 iterations out) over the BP stage (triage + "
+                                   "BP kernel)"},
+            "triage": {"avg_launch_ms": float(pre_ms.mean()),
+                       "achieved": tri_bytes / (float(pre_ms.mean()) * 1e-3) / 1e9 if pre_ms.mean() > 0 else None,
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "bytes_model": f"{TRIAGE_BYTES_PER_SHOT} B per shot: syndrome + readout rows read once"},
             "per_point": per_point,
             "ssf_kernel": ssf_kernel, "ssf_avg_launch_ms": float(ssf_ms.mean()),
-            "isolated_step_ms": float(bp_ms.sum(axis=1).mean() + ssf_ms.sum(axis=1).mean())}
+            "isolated_step_ms": float(stage_ms.sum(axis=1).mean() + ssf_ms.sum(axis=1).mean())}
 
 
 def launch_children(args) -> int:
@@ -288,6 +309,162 @@ def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
     return res
 
 
+def c4_line(dev, shots: int = 1 << 17, ps=(0.01, 0.03), precisions=("f64", "f32")):
+    """BASELINE config 4's code on one GPU (the driver's record of it; the
+    config itself shards 1e7 shots over 8 GPUs exactly as the headline does):
+    biregular_hgp(80, 3, 4, seed=2025), n = 10^4 (reference-generated checks,
+    tests/golden/hgp_80_3_4_s2025_checks.npz; logicals fixture from
+    tools/fixtures/make_c4_logicals.py), R = 0, BP min-sum max_iter 50 + SSF +
+    logical check.  Per (precision, p): one warmup launch and one timed launch
+    of `shots` device-sampled shots, HIP events around the BP and SSF kernels.
+    f64 runs the slot-group kernel (messages stream through HBM: HBM roofline,
+    32 B per edge per shot-iteration + I/O); f32 runs the LDS-resident kernel
+    (every message on chip: LDS roofline, per shot-iteration 20 B per edge --
+    16 B state gather + 4 B v2c scatter -- and 48 B per check -- 32 B row read +
+    16 B state write)."""
+    import scipy.sparse as sp
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+
+    def csr(path, key):
+        d = np.load(os.path.join(REPO, "tests", "golden", path))
+        return sp.csr_matrix((np.ones(d[key + "_indices"].size, np.uint8), d[key + "_indices"], d[key + "_indptr"]),
+                             shape=tuple(d[key + "_shape"]))
+    hz, hx = csr("hgp_80_3_4_s2025_checks.npz", "hz"), csr("hgp_80_3_4_s2025_checks.npz", "hx")
+    lz = csr("hgp_80_3_4_s2025_logicals.npz", "lz")
+    m, n = hz.shape
+    E = int(hz.nnz)
+    lines = []
+    for p in ps:
+        sampler = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, device=dev.index)
+        syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
+        rd = torch.empty((2, shots, n), dtype=torch.uint8, device=dev)
+        for b in range(2):
+            sampler.sample_storage_device(0, p, p, SEED, 200, b * shots, shots, syn[b], rd[b])
+        for prec in precisions:
+            dec = Decoder(hz, 2 * p / 3, method="ms", precision=prec, max_iter=50, flip_sets=hx, logicals=lz,
+                          device=dev.index)
+            iters = torch.empty((2, shots), dtype=torch.int32, device=dev)
+            status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+            fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+            steps = torch.empty((2, shots), dtype=torch.int32, device=dev)
+            dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0],
+                              ssf_steps=steps[0])
+            torch.cuda.synchronize(dev)
+            dec.set_timing(1)
+            t0 = time.perf_counter()
+            dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1],
+                              ssf_steps=steps[1])
+            torch.cuda.synchronize(dev)
+            wall = time.perf_counter() - t0
+            bp_ms, ssf_ms = dec.read_timing()
+            kern = dec.last_kernels()
+            it_sum = int(iters[1].to(torch.int64).sum().item())
+            io = shots * (m + n + 1 + 1 + 4)
+            if "group" in kern[0]:
+                algo = 32 * E * it_sum + io
+                roof = {"bound": "hbm", "peak": HBM_PEAK_GBS,
+                        "bytes_model": "32 B per edge per shot-iteration (f64 messages through HBM: v2c read + c2v "
+                                       "write, c2v read + v2c write) + per-shot I/O"}
+            else:
+                algo = (20 * E + 48 * m) * it_sum
+                roof = {"bound": "lds", "peak": LDS_PEAK_GBS,
+                        "bytes_model": "LDS: 20 B per edge + 48 B per check per shot-iteration (state gather + v2c "
+                                       "scatter; row read + state write)"}
+            ach = algo / (float(bp_ms[0]) * 1e-3) / 1e9
+            roof.update({"achieved": ach, "unit": "GB/s", "frac": ach / roof["peak"], "algorithmic_bytes_per_launch": algo,
+                         "traffic": None})
+            lines.append({"precision": prec, "p": p, "shots": shots, "shots_per_s": shots / wall,
+                          "bp_kernel": kern[0], "ssf_kernel": kern[1], "bp_kernel_ms": float(bp_ms[0]),
+                          "ssf_kernel_ms": float(ssf_ms[0]), "mean_bp_iters": it_sum / shots,
+                          "bp_converged_frac": float((status[1] & 1).to(torch.float64).mean().item()),
+                          "ler": float(fail[1].to(torch.float64).mean().item()), "roofline": roof})
+            del dec
+        del syn, rd, sampler
+        torch.cuda.empty_cache()
+    return {"config": "C4: biregular_hgp(80,3,4,seed=2025), n=10000 (BASELINE configs[3]'s code; 1 GPU, the "
+                      "headline's shot sharding carries it to 8), R=0, BP min-sum max_iter 50 + SSF + logical check, "
+                      f"{shots} device-sampled shots per timed launch", "m": m, "n": n, "E": E, "lines": lines}
+
+
+def reference_default_line(dev, code, shots: int = 1 << 18, batch: int = 1 << 16, p: float = 0.01,
+                           cpu_shots: int = 10000, cpu: bool = True):
+    """The reference's own default decode (BASELINE configs[0]: scripts/p_sweep.py
+    -> misc/p_sweep.py:57-78 defaults, _experiment.py:62-83,213-229): R = 1,
+    decoder_mode bposd, product-sum BP, max_iter = n = 225, OSD-CS order 7,
+    priors 2p/3, f64 BP (ldpc's message precision), through this package's
+    p_sweep pipeline (BatchPipeline: BP kernel on H_st 216 x 558, OSD on the
+    device for BP failures, fold + logical check).  GPU shots/s over `shots`
+    device-sampled shots in `batch`-shot runs; BP time from the BP decoder's HIP
+    events, OSD + the rest = the remainder.  CPU leg: the oracle's restatement of
+    the same loop (oracle/harness_py.spacetime_bposd_corrections: the C ldpc-v1
+    BP restatement on 16 host threads + the numpy OSD restatement) on the first
+    `cpu_shots` of the same syndromes, BP and OSD timed apart, failure flags
+    compared shot by shot."""
+    import torch
+    from exp_ldpc_amd.experiment import BatchPipeline
+    from exp_ldpc_amd.noise_model import depolarizing_noise
+    from exp_ldpc_amd.storage_sim import build_storage_simulation
+    R = 1
+    opts = {"max_iter": code.checks.num_qubits, "bp_method": "ps", "ms_scaling_factor": 0, "osd_method": "osd_cs",
+            "osd_order": 7}
+    priors = (2 * p / 3, 2 * p / 3)
+    noise = depolarizing_noise(p, p)
+    pipe = BatchPipeline(code, R, "bposd", opts, priors, noise=noise, precision="f64", device=dev.index)
+    sim = build_storage_simulation(R, noise, code)
+    nb = max(1, shots // batch)
+    batches = [sim.sample_device(pipe.sampler_graph, batch, SEED, 300, b * batch) for b in range(nb)]
+    first = pipe.run(*batches[0])  # warmup (also the shots the CPU leg decodes)
+    torch.cuda.synchronize(dev)
+    pipe.st.set_timing(nb)
+    t0 = time.perf_counter()
+    fails = conv = 0
+    for syn, rd in batches:
+        r = pipe.run(syn, rd)
+        fails += int(r.fail.sum())
+        conv += r.bp_converged
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    bp_ms, _ = pipe.st.read_timing()
+    total = nb * batch
+    res = {"config": "BASELINE configs[0] path (reference default): (3,4)-HGP n=225, R=1 (H_st 216x558), bposd, "
+                     f"BP product-sum f64 max_iter {opts['max_iter']}, OSD-CS order 7, priors 2p/3, p={p}",
+           "kernel": pipe.st.last_kernels()[0], "shots": total, "shots_per_s": total / wall,
+           "ms_per_batch": wall / nb * 1e3, "batch": batch, "bp_ms_per_batch": float(bp_ms.mean()),
+           "osd_and_rest_ms_per_batch": wall / nb * 1e3 - float(bp_ms.mean()),
+           "bp_converged_frac": conv / total, "ler": fails / total}
+    if cpu:
+        from oracle import load as load_oracle
+        from oracle.harness_py import _fold, _opts, _spacetime_matrix, logical_failures
+        from oracle.osd_py import osd_decode
+        orc = load_oracle()
+        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 64))
+        syn_h = batches[0][0][:cpu_shots].cpu().numpy()
+        rd_h = batches[0][1][:cpu_shots].cpu().numpy()
+        Hst, prior = _spacetime_matrix(code.checks.z, R, *priors)
+        kw = _opts(opts, "f64")
+        t0 = time.perf_counter()
+        out = orc.decode(Hst, prior, syn_h, method="ps", precision="f64", max_iter=kw["max_iter"], ms_scaling=0.0,
+                         want_llr=True, nthreads=threads)
+        t_bp = time.perf_counter() - t0
+        x = out["x"].copy()
+        bad = np.nonzero((out["status"] & 1) == 0)[0]
+        t0 = time.perf_counter()
+        for b in bad:
+            x[b] = osd_decode(Hst, syn_h[b], out["llr"][b], "osd_cs", 7)[1]
+        t_osd = time.perf_counter() - t0
+        corr = _fold(x, code.checks.z.shape[1], R)
+        cpu_fail = logical_failures(code.logicals.z, rd_h, corr)
+        res["cpu_baseline"] = {"value": cpu_shots / (t_bp + t_osd), "unit": "shots/s", "cores": threads, "kind": "port",
+                               "sample": f"the first {cpu_shots} of the GPU run's shots; oracle BP (C, OpenMP) "
+                                         f"{t_bp:.2f} s + numpy OSD-CS 7 on {bad.size} BP failures {t_osd:.2f} s",
+                               "bp_s": t_bp, "osd_s": t_osd,
+                               "fail_flags_identical": bool(np.array_equal(cpu_fail, first.fail[:cpu_shots]))}
+    del batches, pipe
+    torch.cuda.empty_cache()
+    return res
+
+
 class FakeDecoder:
     """--fake-device (CPU tests of the launcher and the rank merge only): a
     stand-in with the decode_device signature; shot s fails iff (s + point) is odd."""
@@ -315,6 +492,9 @@ class FakeDecoder:
 
     def read_timing(self):
         return np.full(self.cap, 1e-3), np.full(self.cap, 1e-3)
+
+    def read_timing_detail(self):
+        return np.zeros(self.cap), np.full(self.cap, 1e-3), np.full(self.cap, 1e-3), np.full(self.cap, -1)
 
 
 class Run:
@@ -415,7 +595,8 @@ class Run:
             self.step(decs, s, streams)
         self.sync()
         self.barrier()
-        return max_time(time.perf_counter() - t0)
+        self.local_elapsed = time.perf_counter() - t0  # this rank's own time (rank 0 reports every rank's)
+        return max_time(self.local_elapsed)
 
     def counts(self):
         """Failures / BP-converged per point over the timed steps, summed over ranks."""
@@ -456,6 +637,9 @@ def main():
     ap.add_argument("--no-sample-phase", action="store_true", help="skip the sampling+decode phase")
     ap.add_argument("--no-large-code", action="store_true",
                     help="skip the config-5 HBM-roofline line (large_code_roofline; rank 0, N=1 only)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the config-4 code line (c4_line; rank 0, N=1 only)")
+    ap.add_argument("--no-reference-default", action="store_true",
+                    help="skip the reference-default bposd line (reference_default_line; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     args.iso_steps = max(1, min(args.iso_steps, args.steps))
@@ -521,6 +705,9 @@ def main():
     elapsed = run.timed(decs, args.steps, run.streams)
     run.pipelined(decs, False)
     fails, conv, itp, ssp = run.counts()
+    # per-rank record of the headline phase: a straggler, a shared device or a
+    # missing rank is visible in rank 0's line
+    rank_rows = gather_rows([rank, -1 if fake else dev.index, run.local_elapsed, args.steps * args.batch * len(ps)])
     shots_per_point = args.steps * args.batch * world
     total_shots = shots_per_point * P
 
@@ -544,14 +731,18 @@ def main():
             d.set_timing(args.iso_steps)
         run.timed(dset, args.iso_steps, run.streams[:1], warm=False)  # every launch is timed
         bp_ms = np.zeros((args.iso_steps, P))
+        pre_ms = np.zeros((args.iso_steps, P))
         ssf_ms = np.zeros((args.iso_steps, P))
+        listed = np.zeros((args.iso_steps, P), np.int64)
         for pi, d in enumerate(dset):
-            a, c = d.read_timing()
-            bp_ms[:, pi] = a[:args.iso_steps]
-            ssf_ms[:, pi] = c[:args.iso_steps]
+            t_pre, t_bp, t_ssf, n_list = d.read_timing_detail()
+            pre_ms[:, pi] = t_pre[:args.iso_steps]
+            bp_ms[:, pi] = t_bp[:args.iso_steps]
+            ssf_ms[:, pi] = t_ssf[:args.iso_steps]
+            listed[:, pi] = n_list[:args.iso_steps]
         it_iso = run.iters[args.warmup:args.warmup + args.iso_steps].to(torch.int64).sum(dim=2).cpu().numpy()
         names = ("", "", "") if fake else dset[-1].last_kernels()  # the instantiations the isolated phase ran
-        iso[prec] = (bp_ms, ssf_ms, it_iso, names)
+        iso[prec] = (bp_ms, ssf_ms, it_iso, names, pre_ms, listed)
 
     # ---- phase 4: sampling + decode in the timed region ----
     sd = None
@@ -559,9 +750,13 @@ def main():
         sd_elapsed = run.timed(decs, args.steps, run.streams[:1], sampler=decs[0], warm=False)
         sd = total_shots / sd_elapsed
 
-    large = None
+    large = c4 = refdef = None
     if rank == 0 and world == 1 and not fake and not args.no_large_code:
         large = large_code_roofline(dev)
+    if rank == 0 and world == 1 and not fake and not args.no_c4:
+        c4 = c4_line(dev)
+    if rank == 0 and world == 1 and not fake and not args.no_reference_default:
+        refdef = reference_default_line(dev, code, cpu=not args.no_cpu_baseline)
 
     if rank == 0:
         value = total_shots / elapsed
@@ -576,6 +771,7 @@ def main():
                    "wilson95": list(w_h), "bp_converged_frac": float(conv[pi] / shots_per_point),
                    "mean_bp_iters_rank0": float(itp[pi]), "mean_ssf_steps_rank0": float(ssp[pi]),
                    "bp_kernel_ms_isolated": float(iso[args.precision][0][:, pi].mean()),
+                   "triage_ms_isolated": float(iso[args.precision][4][:, pi].mean()),
                    "ssf_kernel_ms_isolated": float(iso[args.precision][1][:, pi].mean())}
             cw = None
             if cpu is not None:
@@ -593,11 +789,11 @@ def main():
                 row[variant[0]] = vr
             ler[key] = row
 
-        bp_ms, ssf_ms, it_iso, (bp_kernel, ssf_kernel, pre_kernel) = iso[args.precision]
-        roof = lds_roofline(bp_ms, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms)
+        bp_ms, ssf_ms, it_iso, (bp_kernel, ssf_kernel, pre_kernel), pre_ms, listed = iso[args.precision]
+        roof = lds_roofline(bp_ms, pre_ms, listed, it_iso, args, hz, bp_kernel, ssf_kernel, ssf_ms)
         if pre_kernel:
             roof["pre_kernel"] = pre_kernel
-            roof["timing"] += f"; the BP launch time includes its shot-triage pass {pre_kernel}"
+            roof["triage"]["kernel"] = pre_kernel
         pmc = None if fake else pmc_ceilings(bp_kernel)
         if pmc is not None:
             src, name, k = pmc
@@ -632,7 +828,7 @@ def main():
                        "wave_waves_per_cu": {k: (v or "default") for k, v in occ.items()}},
         }
         if variant:
-            vb, vs, _, _ = iso[variant[0]]
+            vb, vs = iso[variant[0]][0], iso[variant[0]][1]
             result["variants"] = [{"dtype": variant[0], "value": total_shots / variant[1],
                                    "ms_per_step": variant[1] / args.steps * 1e3,
                                    "bp_kernel_ms_isolated_avg": float(vb.mean()),
@@ -641,9 +837,16 @@ def main():
         if sd is not None:
             result["sample_and_decode"] = {"value": sd, "unit": "shots/s", "dtype": args.precision, "streams": 1,
                                            "note": "on-device sampling inside the timed region, one stream"}
+        result["ranks"] = [{"rank": int(r[0]), "device": int(r[1]), "timed_s": r[2], "shots": int(r[3]),
+                            "shots_per_s": r[3] / r[2] if r[2] > 0 else None} for r in rank_rows]
+        result["ranks_seen"] = len(rank_rows)
         result["roofline"] = roof
         if large is not None:
             result["large_code_roofline"] = large
+        if c4 is not None:
+            result["c4_line"] = c4
+        if refdef is not None:
+            result["reference_default"] = refdef
         if cpu is not None:
             result["cpu_baseline"] = cpu
         result["ler"] = ler

@@ -41,7 +41,11 @@ class QdParams(C.Structure):
 
 
 class QdecError(RuntimeError):
-    pass
+    """A failed library call; rc is its status (<= -100: a HIP error)."""
+
+    def __init__(self, msg: str, rc: int = 0):
+        super().__init__(msg)
+        self.rc = rc
 
 
 _p = C.c_void_p
@@ -72,6 +76,7 @@ SIGNATURES = {
     "qd_graph_set_ssf_stream": (_i32, [_p, _p]),
     "qd_graph_set_wave_occupancy": (_i32, [_p, _i32]),
     "qd_graph_read_timing": (_i32, [_p, _p, _p, _i32, C.POINTER(_i32)]),
+    "qd_graph_read_timing_detail": (_i32, [_p, _p, _p, _p, _p, _i32, C.POINTER(_i32)]),
     "qd_graph_last_kernels": (_i32, [_p, C.c_char_p, _i32, C.c_char_p, _i32, C.c_char_p, _i32]),
     "qd_osd_device_supported": (_i32, [_p]),
     "qd_osd_batch_device": (_i32, [_p, _i32, _i32, _i64, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
@@ -117,7 +122,7 @@ def load(path: str | None = None) -> C.CDLL:
 def check(rc: int, what: str = "qdec call") -> None:
     if rc != 0:
         msg = load().qd_last_error()
-        raise QdecError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        raise QdecError(f"{what} failed ({rc}): {msg.decode() if msg else ''}", rc)
 
 
 def ptr(a) -> C.c_void_p | None:

@@ -100,9 +100,14 @@ struct qd_graph {
     // HBM message scratch for the workgroup kernels on graphs too large for LDS
     void* mws = nullptr;
     size_t mws_bytes = 0;
+    size_t mws_failed = 0;  // smallest scratch size whose allocation failed (0: none)
     // kernel timing ring (qd_graph_set_timing): 3 events per decode call
-    std::vector<hipEvent_t> tev;
+    std::vector<hipEvent_t> tev;  // 4 per call (record_ev)
     int t_cap = 0, t_count = 0;
+    // per timed call: compact-list length of a two-pass launch (summed segment
+    // counters, copied into pinned memory behind the launch), -1 otherwise
+    uint64_t* t_listed = nullptr;  // [t_cap][kCmpSegs], hipHostMalloc
+    std::vector<int> t_cmp;
     // min-sum wave kernel: variable (column) held by each lane slot, -1 for pads
     std::vector<int> ms_var_of_slot;
     // workspace chain: every device-buffer decode records ws_ev on its stream after
@@ -230,8 +235,7 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
         // f64: the transfer of a ds_write_b64 takes 6 cycles but every array
         // cycle beyond 4 is a bank-conflict cycle the CU's other waves wait
         // for (PMC: the array is the busiest unit), so the floor is 4
-        constexpr bool v1 = false;  // round-2 layout (tools/dev/patches/r05_pruned_knobs.patch restores the switch)
-        const int ngl = p == 1 ? 2 : 4, ncl = p == 1 ? 32 : 16, floor_c = p == 1 ? 4 : (v1 ? 6 : 4);
+        const int ngl = p == 1 ? 2 : 4, ncl = p == 1 ? 32 : 16, floor_c = 4;
         const int lanes_per = 64 / ngl;
         std::vector<int> grp(E), lg(E), pos(E);
         for (int i = 0; i < m; ++i)
@@ -352,7 +356,7 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
                 return mx;
             };
             const int wl = p == 1 ? 16 : 8;  // state-write group width = classes
-            const int NW = v1 ? 0 : g.m_pad / wl;
+            const int NW = g.m_pad / wl;
             auto wcost = [&](int w) {
                 int cnt[16] = {0};
                 int mx = 0;
@@ -370,8 +374,7 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
             const int iters = 60000;
             std::vector<int> aff;
             std::vector<int> newc;
-            // v1 moves real checks only (pads take the free slots afterwards)
-            const int nmov = v1 ? m : g.m_pad;
+            const int nmov = g.m_pad;
             for (int it = 0; it < iters; ++it) {
                 const double T = 0.6 * (1.0 - (double)it / iters) + 0.02;
                 const int c1 = (int)(rng() % (unsigned)nmov);
@@ -413,22 +416,10 @@ void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
             }
             sst = best;
         }
+        // pad check lanes write zeros into their own slots (min-sum of an empty
+        // row never reaches them: their rows hold Big)
         std::vector<uint16_t> ss16(g.m_pad, (uint16_t)g.m_pad);
-        if (!v1) {
-            // pad check lanes write zeros into their own slots (min-sum of an
-            // empty row never reaches them: their rows hold Big)
-            for (int i = 0; i < g.m_pad; ++i) ss16[i] = (uint16_t)sst[i];
-        } else {
-            for (int i = 0; i < m; ++i) ss16[i] = (uint16_t)sst[i];
-            std::vector<char> used(g.m_pad + 1, 0);
-            for (int i = 0; i < m; ++i) used[sst[i]] = 1;
-            int f = 0;
-            for (int i = m; i < g.m_pad; ++i) {
-                while (used[f]) ++f;
-                ss16[i] = (uint16_t)f;
-                used[f] = 1;
-            }
-        }
+        for (int i = 0; i < g.m_pad; ++i) ss16[i] = (uint16_t)sst[i];
         g.ms_sslot[p] = G->arena.upload(ss16);
         std::vector<uint32_t> etab((size_t)kDC * g.n_pad);
         for (int gi = 0; gi < NG; ++gi) {
@@ -797,6 +788,14 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
     size_t need = block_scratch_bytes(G->dg, method, precision, G->num_cus, a);
     *bytes = need;
     if (need == 0) return nullptr;
+    const size_t floor = block_scratch_floor(G->dg, method, precision, G->num_cus, a);
+    // capped after an allocation failure: a request at or above the size that
+    // failed keeps the reduced scratch (the launch sizes its grid from the bytes
+    // it gets) instead of draining and failing the same allocation every call
+    if (need > G->mws_bytes && G->mws && G->mws_failed && need >= G->mws_failed && G->mws_bytes >= floor) {
+        *bytes = G->mws_bytes;
+        return G->mws;
+    }
     if (need > G->mws_bytes) {
         ws_drain(G);  // launches still in flight may use the old scratch
         if (G->mws) hip_check(hipFree(G->mws), "hipFree scratch");
@@ -804,7 +803,6 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
         G->mws_bytes = 0;
         // on an allocation failure, halve the slot groups in flight down to one
         // (the launch sizes its grid from the bytes it gets; results do not change)
-        const size_t floor = block_scratch_floor(G->dg, method, precision, G->num_cus, a);
         for (;;) {
             const hipError_t e = hipMalloc(&G->mws, need);
             if (e == hipSuccess) break;
@@ -812,6 +810,7 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
             G->mws = nullptr;
             if (e != hipErrorOutOfMemory || need <= floor)
                 hip_check(e, "hipMalloc message scratch");
+            G->mws_failed = G->mws_failed ? std::min(G->mws_failed, need) : need;
             need = std::max(floor, floor + (need - floor) / 2);
         }
         G->mws_bytes = need;
@@ -829,12 +828,28 @@ void note_kernels(qd_graph* G) {
 
 void attach_timing(qd_graph* G, DecodeArgs& a) {
     a.ev = nullptr;
-    if (G->t_cap > 0 && G->t_count < G->t_cap) a.ev = &G->tev[(size_t)3 * G->t_count++];
+    if (G->t_cap > 0 && G->t_count < G->t_cap) a.ev = &G->tev[(size_t)4 * G->t_count++];
+}
+
+// after a timed launch: the compact list's length (the triage's segment
+// counters, one per 128-B line) into the call's pinned slot, on the BP stream
+void note_listed(qd_graph* G, const DecodeArgs& a, hipStream_t s) {
+    if (!a.ev || !G->t_listed) return;
+    const size_t slot = (size_t)(a.ev - G->tev.data()) / 4;
+    const bool cmp = !G->last_pre.empty() && a.cmp_count;
+    G->t_cmp[slot] = cmp ? 1 : 0;
+    if (cmp)
+        hip_check(hipMemcpy2DAsync(G->t_listed + slot * kCmpSegs, 8, a.cmp_count, 128, 8, kCmpSegs,
+                                   hipMemcpyDeviceToHost, s),
+                  "hipMemcpy2DAsync list counters");
 }
 
 void free_timing(qd_graph* G) {
     for (hipEvent_t e : G->tev) (void)hipEventDestroy(e);
     G->tev.clear();
+    if (G->t_listed) (void)hipHostFree(G->t_listed);
+    G->t_listed = nullptr;
+    G->t_cmp.clear();
     G->t_cap = G->t_count = 0;
 }
 
@@ -1421,6 +1436,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
+        note_listed(G, a, s);
         // the last user of the queue is the SSF kernel: the workspace chain
         // continues on its stream (the next decode on this handle waits for it)
         ws_release(G, split ? G->ssf_stream : s);
@@ -1480,6 +1496,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
+        note_listed(G, a, s);
         ws_release(G, s);
         auto d2h = [&](void* h, const Reg& r, const char* what) {
             if (h) hip_check(hipMemcpyAsync(h, dptr(r), r.bytes, hipMemcpyDeviceToHost, s), what);
@@ -1582,8 +1599,14 @@ int qd_graph_set_timing(qd_graph* G, int32_t capacity) {
         set_device(G);
         if (capacity < 0) throw Fail(-90, "negative timing capacity");
         free_timing(G);
-        G->tev.resize((size_t)3 * capacity);
+        G->tev.resize((size_t)4 * capacity);
         for (auto& e : G->tev) hip_check(hipEventCreate(&e), "hipEventCreate");
+        if (capacity > 0) {
+            void* h = nullptr;
+            hip_check(hipHostMalloc(&h, (size_t)capacity * kCmpSegs * 8, hipHostMallocDefault), "hipHostMalloc");
+            G->t_listed = static_cast<uint64_t*>(h);
+            G->t_cmp.assign(capacity, 0);
+        }
         G->t_cap = capacity;
         G->t_count = 0;
     });
@@ -1596,13 +1619,45 @@ int qd_graph_read_timing(qd_graph* G, float* bp_ms, float* ssf_ms, int32_t max_c
         if (!n_calls) throw Fail(-91, "null n_calls");
         const int n = std::min(G->t_count, std::max(0, max_calls));
         for (int i = 0; i < n; ++i) {
-            hipEvent_t* e = &G->tev[(size_t)3 * i];
+            hipEvent_t* e = &G->tev[(size_t)4 * i];
             hip_check(hipEventSynchronize(e[2]), "hipEventSynchronize");
             float t0 = 0, t1 = 0;
             hip_check(hipEventElapsedTime(&t0, e[0], e[1]), "hipEventElapsedTime");
             hip_check(hipEventElapsedTime(&t1, e[1], e[2]), "hipEventElapsedTime");
             if (bp_ms) bp_ms[i] = t0;
             if (ssf_ms) ssf_ms[i] = t1;
+        }
+        *n_calls = n;
+        G->t_count = 0;
+    });
+}
+
+int qd_graph_read_timing_detail(qd_graph* G, float* pre_ms, float* bp_ms, float* ssf_ms, int64_t* listed,
+                                int32_t max_calls, int32_t* n_calls) {
+    return guarded([&] {
+        check_graph(G);
+        set_device(G);
+        if (!n_calls) throw Fail(-91, "null n_calls");
+        const int n = std::min(G->t_count, std::max(0, max_calls));
+        for (int i = 0; i < n; ++i) {
+            hipEvent_t* e = &G->tev[(size_t)4 * i];
+            hip_check(hipEventSynchronize(e[2]), "hipEventSynchronize");
+            hip_check(hipEventSynchronize(e[1]), "hipEventSynchronize");
+            float t0 = 0, t1 = 0, t2 = 0;
+            hip_check(hipEventElapsedTime(&t0, e[0], e[3]), "hipEventElapsedTime");
+            hip_check(hipEventElapsedTime(&t1, e[3], e[1]), "hipEventElapsedTime");
+            hip_check(hipEventElapsedTime(&t2, e[1], e[2]), "hipEventElapsedTime");
+            if (pre_ms) pre_ms[i] = t0;
+            if (bp_ms) bp_ms[i] = t1;
+            if (ssf_ms) ssf_ms[i] = t2;
+            if (listed) {
+                int64_t c = -1;
+                if (G->t_cmp[i]) {
+                    c = 0;
+                    for (int k = 0; k < kCmpSegs; ++k) c += (int64_t)G->t_listed[(size_t)i * kCmpSegs + k];
+                }
+                listed[i] = c;
+            }
         }
         *n_calls = n;
         G->t_count = 0;

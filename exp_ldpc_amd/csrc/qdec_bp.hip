@@ -305,33 +305,16 @@ __global__ __launch_bounds__(64) void bp_wave_kernel(DevGraph g, DecodeArgs a) {
 //      (spec: ties -> lowest g, then lowest subset bitmask),
 //   4. the flip updates the residual (u32 per check in LDS) and hard decision.
 // Key (int32): score << 15 | (127 - g) << 8; |score| <= 32*840 < 2^15, g < 128.
-#ifndef QDEC_SSF_WAVES
-#define QDEC_SSF_WAVES 4  // waves per workgroup sharing the generator tables
-#endif
-constexpr int kSsfWaves = QDEC_SSF_WAVES;
-#ifndef QDEC_SSF_INV_INIT
-#define QDEC_SSF_INV_INIT 0  // 1: first-step local syndromes from the inverse table (measured no faster)
-#endif
+constexpr int kSsfWaves = 4;  // waves per workgroup sharing the generator tables
 // Registers are budgeted for 5 waves per SIMD (<= 96 VGPRs, ~40 dwords of the
-// shot setup / finalisation spilled): with the u8 residual (QDEC_SSF_RES8) five
-// 4-wave workgroups fit a CU's LDS.  Measured against 4 per SIMD with the u32
-// residual, interleaved: isolated SSF sum 6.57-6.59 vs 6.76-6.78 ms, headline
-// 87.7-89.2 vs 85.8-86.5 M shots/s (the smaller LDS footprint also co-resides
-// better with the concurrent BP kernels).
-#ifndef QDEC_SSF_OCC
-#define QDEC_SSF_OCC 5  // minimum waves per SIMD the SSF kernel is compiled for
-#endif
-#ifndef QDEC_SSF_RES32
-#define QDEC_SSF_RES8
-#endif
+// shot setup / finalisation spilled): with the u8 residual five 4-wave
+// workgroups fit a CU's LDS.  Measured against 4 per SIMD with a u32 residual,
+// interleaved: isolated SSF sum 6.57-6.59 vs 6.76-6.78 ms, headline 87.7-89.2 vs
+// 85.8-86.5 M shots/s (the smaller LDS footprint also co-resides better with the
+// concurrent BP kernels).
+constexpr int kSsfOcc = 5;  // minimum waves per SIMD the SSF kernel is compiled for
+using SsfRes = uint8_t;     // residual bit per check
 
-// residual bit per check: u8 (QDEC_SSF_RES8, the default: 3/4 less LDS per wave
-// than u32, so five 4-wave workgroups fit a CU) or u32 (QDEC_SSF_RES32)
-#ifdef QDEC_SSF_RES8
-using SsfRes = uint8_t;
-#else
-using SsfRes = uint32_t;
-#endif
 template <int RG>
 struct SsfLds {
     static constexpr int GP = 64 * RG;
@@ -358,7 +341,7 @@ struct SsfLds {
 // XW/RW: words of the packed queue entries (hard decision by column, residual
 // by check) written by the wave BP kernels (queue_push_packed).
 template <int RG, int XW, int RW>
-__global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64 * kSsfWaves, kSsfOcc) void ssf_wave_kernel(DevGraph g, DecodeArgs a) {
     constexpr int GP = SsfLds<RG>::GP;
     constexpr int QW = QEntry<XW, RW>::QW;
     static_assert(2 * QW <= 64, "entry staging");
@@ -414,7 +397,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
     const bool want_fail = a.fail && a.readout && g.k > 0;
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
     // the split scorer enumerates hi < 8 per lane (generators of up to 8 qubits
-    // have nhi <= 16, half <= 8); QDEC_SSF_NOSPLIT=1 at launch disables it
+    // have nhi <= 16, half <= 8); QD_SSF_SCAN_NOSPLIT disables it
     const bool split_ok = nhi <= 16 && !a.ssf_nosplit;
     const int nlcw = (g.g_nlcmax + 3) / 4;
     QDEC_STAMP_DECL
@@ -458,34 +441,6 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             sres[i] = i < m ? (SsfRes)((R[w] >> lane) & 1) : (SsfRes)0;
             sw += __popcll(R[w]);
         }
-        // QDEC_SSF_INV_INIT (incremental mode): the first step's local syndromes
-        // from the inverse table too, fanned out from the violated checks (listed
-        // into slt, which step 1 overwrites) instead of gathered bit by bit (up
-        // to kGenLC LDS reads per generator).  Bit-exact, measured no faster
-        // (isolated SSF sum 6.79-6.83 vs 6.74-6.76 ms), so off.
-        constexpr bool kInvInit = QDEC_SSF_INV_INIT && RW <= RG;  // slt holds GP >= 64 * RW check ids
-        const bool inv_init = inc && kInvInit;
-        if (inv_init) {
-            int nv = 0;
-#pragma unroll
-            for (int rg = 0; rg < RG; ++rg) slc[rg * 64 + lane] = 0u;
-#pragma unroll
-            for (int w = 0; w < RW; ++w) {
-                const int i = w * 64 + lane;
-                const bool v = i < m && ((R[w] >> lane) & 1);
-                const unsigned long long bal = __ballot(v);
-                if (v)
-                    slt[nv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = (uint32_t)i;
-                nv += __popcll(bal);
-            }
-            wave_lds_sync();
-            const int npair = nv << g.g_invl;
-            for (int pr = lane; pr < npair; pr += 64) {
-                const uint32_t e = invt[(slt[pr >> g.g_invl] << g.g_invl) + (pr & (g.g_invd - 1))];
-                if (e != 0xffffu) atomicXor(&slc[e & 0xff], 1u << (e >> 8));
-            }
-        }
         wave_lds_sync();
         uint32_t slo[RG];
         int steps = 0;
@@ -499,7 +454,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
             for (int rg = 0; rg < RG; ++rg) {
                 const int gi = rg * 64 + lane;
                 uint32_t sl = 0;
-                if (!inc || (first && !inv_init)) {
+                if (!inc || first) {
 #pragma unroll
                     for (int wq = 0; wq < NLW; ++wq) {
                         if (wq < nlcw) {
@@ -691,9 +646,7 @@ __global__ __launch_bounds__(64 * kSsfWaves, QDEC_SSF_OCC) void ssf_wave_kernel(
 // kernel's gather / list / score / pick / apply chain.  The shot's first local
 // syndromes are the toggle rows of its residual's violated checks.
 constexpr int kLutWaves = 16;  // waves per workgroup sharing the tables
-#ifndef QDEC_LUT_OCC
-#define QDEC_LUT_OCC 8         // waves per SIMD the table-driven kernel is compiled for
-#endif
+constexpr int kLutOcc = 8;     // waves per SIMD the table-driven kernel is compiled for (lean build)
 
 struct SsfLutLds {
     static constexpr int kStage = 3;  // packed queue entries staged per wave (two slots ahead)
@@ -716,7 +669,7 @@ struct SsfLutLds {
 // p_sweep's call); otherwise finalize_shot writes x / corr (its registers would
 // push the lean build past 64 VGPRs, 8 waves per SIMD).
 template <int RG, int XW, int RW, bool LEAN>
-__global__ __launch_bounds__(64 * kLutWaves, LEAN ? QDEC_LUT_OCC : 4) void ssf_lut_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_kernel(DevGraph g, DecodeArgs a) {
     static_assert(RG == 1 || RG == 2, "two generators per lane at most (16-bit halves of one word)");
     static_assert(XW <= 32, "hard-decision bits per lane");
     constexpr int QW = QEntry<XW, RW>::QW;
@@ -1010,7 +963,7 @@ static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t str
     const size_t tiles = triage_img_bytes(64 * (int64_t)g.m) + triage_img_bytes(64 * (int64_t)g.n_data);
     const size_t it1 = a.it1_lut ? TriageIt1<RC, RV>::bytes : 0;
     const size_t lds = ((want_fail ? (size_t)g.k * g.lz_words * 8 : 0) + 15) / 16 * 16 +
-                       (QDEC_TRIAGE_BITS ? tiles + it1 : std::max(tiles, it1));
+                       tiles + it1;
     if (lds > 64 * 1024) {  // large logical tables (k <= 256, lz_words <= 9)
         const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ms_triage_kernel<RC, RV>),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1050,6 +1003,7 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             if (e != hipSuccess) return (int)e;
             int rc = launch_triage<RC, RV>(g, b, stream);
             if (rc != 0) return rc;
+            if (b.ev) (void)hipEventRecord(b.ev[3], stream);  // end of the pre-pass
             size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16 + 2 * 64 * 8;
             // a capped grid (f64: 8 waves per CU) must also be placed evenly: the
             // dispatcher stacks up to the kernel's own occupancy on a CU (11 for

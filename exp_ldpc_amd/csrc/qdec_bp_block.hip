@@ -677,34 +677,22 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
 // groups per CU: +30 % on config 5 against 8-wave groups), 8 for f64 (register
 // bound at 2 waves per SIMD either way; 8-wave groups finish and refill slots
 // with twice the threads: config 4 f64 at p = 0.005, 2.9 iterations per shot,
-// 604 k vs 401 k shots/s).  QDEC_GRP_WAVES overrides both (A/B define).
+// 604 k vs 401 k shots/s).
 template <typename T>
 constexpr int grp_waves() {
-#ifdef QDEC_GRP_WAVES
-    return QDEC_GRP_WAVES;
-#else
     return sizeof(T) == 4 ? 4 : 8;
-#endif
 }
 // Checks / columns per wave step: every load of a step is issued before any is
 // used, so a wave keeps UC * DR (check pass) or UV * (column degree) loads of
 // whole 64-slot lines in flight; the column pass has few edges per column, so
-// it takes more columns per step.  (QDEC_GRP_UC / QDEC_GRP_UV: A/B defines.)
+// it takes more columns per step.
 template <typename T, int DR>
 constexpr int grp_uc() {
-#ifdef QDEC_GRP_UC
-    return QDEC_GRP_UC;
-#else
     return sizeof(T) == 4 ? 4 : (DR <= 8 ? 4 : 2);
-#endif
 }
 template <typename T, int DC>
 constexpr int grp_uv() {
-#ifdef QDEC_GRP_UV
-    return QDEC_GRP_UV;
-#else
     return sizeof(T) == 4 ? (DC <= 4 ? 16 : 8) : (DC <= 4 ? 8 : 4);
-#endif
 }
 constexpr int kFinPerCu = 8;          // SSF/finalize workgroups per CU when their state is in HBM
 constexpr size_t kGrpHeader = 256;    // scratch header: the shot counter

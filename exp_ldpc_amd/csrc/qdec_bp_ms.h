@@ -73,8 +73,8 @@ __device__ __forceinline__ double max_abs2_f64(double a, double b) {
     return r;
 }
 
-// Sign-bit tests for f64 messages (QDEC_MS_SIGNBIT, default on; LEAN launches
-// only).  ldpc's sign test `v <= 0` equals v's sign bit for every v but +0.
+// Sign-bit tests for f64 messages (LEAN launches only; the others keep the
+// compares).  ldpc's sign test `v <= 0` equals v's sign bit for every v but +0.
 // The check pass takes its row parity as the XOR of the high dwords (no f64
 // compares) and the variable pass flips a message's sign by the sign bit of the
 // v2c message it sent.  Both differ from the compares only through zero
@@ -86,9 +86,6 @@ __device__ __forceinline__ double max_abs2_f64(double a, double b) {
 // is left open, which changes no `<= 0` test, no magnitude and no hard
 // decision (only the sign of an exactly-zero posterior, which LEAN launches do
 // not output).
-#ifndef QDEC_MS_SIGNBIT
-#define QDEC_MS_SIGNBIT 1
-#endif
 __device__ __forceinline__ uint32_t f64_hi(double x) { return (uint32_t)((unsigned long long)__double_as_longlong(x) >> 32); }
 // x with its sign bit XORed with bit 31 of m: one v_bitop3_b32 on the high
 // dword (table 0x6c = (src0 & src2) ^ src1)
@@ -207,11 +204,9 @@ struct ShotSeq {
 // BP counter chunk (diagnostic define): 8 / 16 trade fewer atomics at low p
 // (p = 0.001: 0.51 -> 0.45 / 0.47 ms per 2^18 shots) for coarser tail balance
 // at high p (p = 0.1: 7.04 -> 7.08 / 7.50 ms); the sweep's sum is flat at 8
-#ifndef QDEC_BP_CHUNK
-#define QDEC_BP_CHUNK 4
-#endif
+    static constexpr int kBpChunk = 4;
     __device__ ShotSeq(const DecodeArgs& a, int lane)
-        : ShotSeq(a.B, a.wave_ctr, blockIdx.x, gridDim.x, lane, QDEC_BP_CHUNK) {}
+        : ShotSeq(a.B, a.wave_ctr, blockIdx.x, gridDim.x, lane, kBpChunk) {}
     // `total` items over `nw` persistent waves, this one being wave `wid`
     __device__ ShotSeq(int64_t total, unsigned long long* counter, int64_t wid, int64_t nw, int lane, int chunk = 4) {
         kChunk = chunk;
@@ -257,7 +252,7 @@ struct MsCore {
     static constexpr int NP = (RV + 1) / 2;
     static constexpr int D3P = D3R & ~1;
     static constexpr int PREC = sizeof(T) == 4 ? 1 : 0;
-    static constexpr bool SB = sizeof(T) == 8 && LEAN && QDEC_MS_SIGNBIT;
+    static constexpr bool SB = sizeof(T) == 8 && LEAN;
 
     uint32_t etab[RV][kDC];      // v2c element | state index << 16 (edges k < kd(rv))
     V2 L[NP];                    // priors of rounds (2p, 2p+1)
@@ -501,51 +496,18 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     int64_t shot = seq.next(lane);
     typename Io::Shift sh = io.stage(g, a, shot, 0, 0, lane);  // row offsets of `shot`'s stage
     int64_t nxt = seq.next(lane);
-    int64_t nxt2 = 0;  // the shot after nxt (stage depth 2)
-    typename Io::Shift sh1;  // ... of nxt's (stage depth 2)
-    if constexpr (Io::kDepth == 2) {
-        sh1 = io.stage(g, a, nxt, 1, 1, lane);
-        nxt2 = seq.next(lane);
-    }
     wave_lds_sync();
 
     int sb = 0, buf = 0;  // syndrome / readout staging buffers of `shot`
-    // QDEC_DEFER_STORES (LEAN + DEFER, stage depth 1): a shot's per-shot outputs
-    // are stored by the next shot, right after its stage, as exactly kDS store
-    // instructions (null outputs and a shot without them go to a sink in the
-    // handle's control block), so that no wait for a later stage also waits for
-    // these stores to be acknowledged; the waits below count them
-    constexpr bool DS = QDEC_DEFER_STORES && LEAN && DEFER && Io::kDepth == 1;
-    constexpr int kDS = DS ? 4 : 0;
-    int64_t p_shot = -1;     // shot whose outputs are pending (-1: none)
-    int p_iters = 0, p_fin = 0, p_fail = 0, p_status = 0;  // p_fin: status / steps / fail pending too
-    uint8_t* const sink = reinterpret_cast<uint8_t*>(a.wave_ctr) + 128;
-    auto flush = [&]() {
-        if constexpr (DS) {
-            const bool v = p_shot >= 0, f = v && p_fin;
-            int32_t* pi = (v && a.iters) ? a.iters + p_shot : reinterpret_cast<int32_t*>(sink);
-            uint8_t* ps = (f && a.status) ? a.status + p_shot : sink + 4;
-            int32_t* pq = (f && a.ssf_steps) ? a.ssf_steps + p_shot : reinterpret_cast<int32_t*>(sink + 8);
-            uint8_t* pf = (f && a.fail) ? a.fail + p_shot : sink + 12;
-            if (lane == 0) {
-                __builtin_nontemporal_store(p_iters, pi);
-                __builtin_nontemporal_store((uint8_t)p_status, ps);
-                __builtin_nontemporal_store(0, pq);
-                __builtin_nontemporal_store((uint8_t)p_fail, pf);
-            }
-        }
-    };
-    flush();  // sink stores: the waits below count kDS stores after every stage, from the first
     QDEC_STAMP_DECL
 #ifdef QDEC_STAMPS
     const unsigned long long qdec_t0 = __builtin_amdgcn_s_memtime(), qdec_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     for (; shot < a.B;) {
-        // ---- syndrome (staged kDepth shots ahead: at least the NR readout loads
-        // of the same stage and the later stages are younger); then stage the
-        // shot kDepth ahead ----
+        // ---- syndrome (staged one shot ahead: at least the NR readout loads of
+        // the same stage are younger); then stage the next shot ----
         QDEC_STAMP(5);
-        wait_vmem<Io::kWaitSyn + kDS>();
+        wait_vmem<Io::kWaitSyn>();
         Io::patch_tail(a.syn, a.B, m, shot, io.syn_area(sb), sh.s, lane);
         wave_lds_sync();
         QDEC_STAMP(0);
@@ -558,9 +520,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         }
         wait_lds();
         const int64_t nn = seq.next(lane);  // any counter request is older than the stage
-        const typename Io::Shift shn = Io::kDepth == 2 ? io.stage(g, a, nxt2, sb, buf == 0 ? 2 : buf - 1, lane)
-                                                       : io.stage(g, a, nxt, 0, buf ^ 1, lane);
-        flush();  // the previous shot's outputs (DS), after the stage
+        const typename Io::Shift shn = io.stage(g, a, nxt, 0, buf ^ 1, lane);
         if (!LEAN && a.syn_flags) {
             const bool use_b = (a.syn_flags & 1) && a.base;
             const bool use_r = (a.syn_flags & 2) && a.readout;
@@ -600,19 +560,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         uint64_t X[RV];
         bool pres[RC];
         int it = 1;
-#ifdef QDEC_CALIB_NOBP
-        // HBM calibration variant (tools/dev/gpu_calib.sh): the same staging,
-        // queue and output traffic with the BP loop compiled out; every shot
-        // "converges" at once with the zero hard decision
-        constexpr bool kSkipBp = true;
-#pragma unroll
-        for (int rv = 0; rv < RV; ++rv) X[rv] = 0ull;
-#pragma unroll
-        for (int rc = 0; rc < RC; ++rc) pres[rc] = sbit[rc];
-#else
-        constexpr bool kSkipBp = false;
-#endif
-        bool conv = kSkipBp;
+        bool conv = false;
         if (skip) {
             conv = true;
 #pragma unroll
@@ -620,7 +568,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
 #pragma unroll
             for (int rc = 0; rc < RC; ++rc) pres[rc] = false;
         }
-        if (!kSkipBp && !skip) conv = core.iterate(a, v2c, st, m, lane, sbit, Q, X, pres, it);
+        if (!skip) conv = core.iterate(a, v2c, st, m, lane, sbit, Q, X, pres, it);
         const int iters = conv ? it : a.max_iter;
         QDEC_STAMP(2);
         QDEC_COUNT(8, iters);
@@ -629,16 +577,10 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         // kWaitRd most recent vector-memory operations are the later shots' stages
         const bool need_rd = a.readout && a.fail && g.k > 0;  // the SSF queue carries it too
         if (need_rd) {
-            wait_vmem<Io::kWaitRd + 2 * kDS>();
+            wait_vmem<Io::kWaitRd>();
             Io::patch_tail(a.readout, a.B, g.n_data, shot, io.rd_area(buf), sh.r, lane);
         }
-        if constexpr (DS) {
-            p_shot = shot;
-            p_iters = iters;
-            p_fin = 0;
-        } else if (lane == 0 && a.iters) {
-            a.iters[shot] = iters;
-        }
+        if (lane == 0 && a.iters) a.iters[shot] = iters;
         // hard decision by column (slot order -> xh[column])
 #pragma unroll
         for (int rv = 0; rv < RV; ++rv) xh[core.col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
@@ -687,11 +629,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
                 for (int w = 0; w < RV; ++w) Xc[w] = __ballot(xh[w * 64 + lane] & 1);
                 any_fail = fail_from_words<RV, !LEAN>(g, a, shot, lane, Xc, io.rd_area(buf) + sh.r, io.lz);
             }
-            if constexpr (DS) {
-                p_fin = 1;
-                p_status = conv ? 3 : 0;
-                p_fail = any_fail;
-            } else if (lane == 0) {
+            if (lane == 0) {
                 if (a.status) a.status[shot] = (uint8_t)(conv ? 3 : 0);
                 if (a.ssf_steps) a.ssf_steps[shot] = 0;
                 if (a.fail) a.fail[shot] = (uint8_t)any_fail;
@@ -702,25 +640,15 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         wave_lds_sync();
         QDEC_STAMP(4);
         shot = nxt;
-        if constexpr (Io::kDepth == 2) {
-            nxt = nxt2;
-            nxt2 = nn;
-            sh = sh1;
-            sh1 = shn;
-            sb ^= 1;
-            buf = buf == 2 ? 0 : buf + 1;
-        } else {
-            nxt = nn;
-            sh = shn;
-            buf ^= 1;
-        }
+        nxt = nn;
+        sh = shn;
+        buf ^= 1;
     }
 #ifdef QDEC_STAMPS
     QDEC_COUNT(10, __builtin_amdgcn_s_memtime() - qdec_t0);
     QDEC_COUNT(11, __builtin_amdgcn_s_memrealtime() - qdec_r0);
     QDEC_COUNT(12, 1);
 #endif
-    flush();  // the last shot's outputs
     QDEC_FLUSH_AT(0);
 }
 
@@ -753,12 +681,9 @@ __device__ __forceinline__ uint32_t byte_bits4(uint32_t d) { return ((d & 0x0101
 // One tile of a shot-major byte buffer, as the 16-B chunks covering bytes
 // [start, start + len) of a buffer of `total` bytes (image chunk 0 = the chunk
 // at or below `start`; `shift` = the byte offset of `start` inside the image).
-// QDEC_TRIAGE_BITS (default): the LDS image keeps only bit 0 of every byte
-// (16 bits per chunk, 1/8 of the bytes), so a tile pair needs ~3 KB of LDS
-// instead of ~21 KB and more tiles are in flight per CU; 0: byte images (A/B).
-#ifndef QDEC_TRIAGE_BITS
-#define QDEC_TRIAGE_BITS 1
-#endif
+// The LDS image keeps only bit 0 of every byte (16 bits per chunk, 1/8 of the
+// bytes), so a tile pair needs ~3 KB of LDS instead of ~21 KB and more tiles
+// are in flight per CU.
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 // bit 0 of 16 bytes as a 16-bit word (byte t -> bit t)
 __device__ __forceinline__ uint32_t chunk_bits16(u32x4 v) {
@@ -768,19 +693,13 @@ struct TileSrc {
     const uint8_t* buf;
     int64_t total, c0;  // c0: first 16-B chunk
     int nch, shift;
-    void* img;          // u32x4 per chunk, or u16 bits per chunk (QDEC_TRIAGE_BITS)
+    void* img;          // u16 bits per chunk
     __device__ TileSrc(const uint8_t* b, int64_t tot, int64_t start, int64_t len, void* dst) : buf(b), total(tot), img(dst) {
         c0 = start >> 4;
         nch = (int)(((start + len + 15) >> 4) - c0);
         shift = (int)(start & 15);
     }
-    __device__ __forceinline__ void put(int c, u32x4 v) const {
-#if QDEC_TRIAGE_BITS
-        static_cast<uint16_t*>(img)[c] = (uint16_t)chunk_bits16(v);
-#else
-        static_cast<u32x4*>(img)[c] = v;
-#endif
-    }
+    __device__ __forceinline__ void put(int c, u32x4 v) const { static_cast<uint16_t*>(img)[c] = (uint16_t)chunk_bits16(v); }
     // chunk c of the image from its bytes (the buffer's last partial chunk)
     __device__ u32x4 bytes(int c) const {
         uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -851,27 +770,6 @@ __device__ __forceinline__ void tile_pair_to_lds(const TileSrc& A, const TileSrc
     }
 }
 
-// NB bytes of a lane's row at byte offset `off` of an LDS dword image, as bit
-// words (bit i of word i/64 = bit 0 of byte i); bytes >= len are cleared.
-template <int NW>
-__device__ __forceinline__ void row_bits(const uint32_t* img, int off, int len, uint64_t (&w)[NW]) {
-#pragma unroll
-    for (int i = 0; i < NW; ++i) w[i] = 0ull;
-    const int q = off >> 2, sh = off & 3;
-    uint32_t lo = img[q];
-#pragma unroll
-    for (int t = 0; t < 16 * NW; ++t) {
-        if (4 * t < len) {
-            const uint32_t hi = img[q + t + 1];
-            // the 4 bytes at off + 4t: ({hi, lo} >> 8 sh)[31:0]
-            uint32_t nib = byte_bits4(__builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh));
-            lo = hi;
-            if (4 * t + 4 > len) nib &= (1u << (len - 4 * t)) - 1u;
-            w[t / 16] |= (uint64_t)nib << (4 * (t % 16));
-        }
-    }
-}
-
 // Iteration 1 in the triage (DecodeArgs::it1_lut), bit-sliced over the tile's
 // 64 shots: the syndrome is transposed to one word per check (bit s = shot s),
 // each column's decision word is its 16-bit table (it1_tables, qdec_abi.cpp)
@@ -886,21 +784,9 @@ struct TriageIt1 {
     static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
 };
 
-#ifndef QDEC_T1_GATE_W
-#define QDEC_T1_GATE_W 12  // iteration-1 tile gate: syndrome weight bound ...
-#endif
-#ifndef QDEC_T1_GATE_N
-#define QDEC_T1_GATE_N 8  // ... and shots of the tile within it (A/B defines)
-#endif
-#ifndef QDEC_TRIAGE_UB
-#define QDEC_TRIAGE_UB 16  // readout-tile loads per lane per round (A/B)
-#endif
-#ifndef QDEC_TRIAGE_PAIR
-#define QDEC_TRIAGE_PAIR 1  // 0: the syndrome tile, then the readout tile (A/B)
-#endif
-#ifndef QDEC_T1_BALLOT
-#define QDEC_T1_BALLOT 0  // 1: transpose by 64 ballots per word (A/B)
-#endif
+constexpr int kT1GateW = 12;  // iteration-1 tile gate: syndrome weight bound ...
+constexpr int kT1GateN = 8;   // ... and shots of the tile within it
+constexpr int kTriageUB = 16;  // readout-tile loads per lane per round
 // 64 x 64 bit transpose across the wave: lane r holds row r (bit c = entry
 // (r, c)), and gets back column r (bit c = entry (c, r)).  Six block-swap
 // stages, each one exchange with lane ^ j: the off-diagonal j x j blocks of
@@ -940,7 +826,7 @@ __device__ __forceinline__ uint64_t lut4_words(uint32_t lut, uint64_t w0, uint64
     return f;
 }
 
-// The same from a bit image (QDEC_TRIAGE_BITS): bit `off` onwards, `len` bits;
+// The same from a bit image: bit `off` onwards, `len` bits;
 // reads up to three dwords past the row's last bit (the image has spares).
 template <int NW>
 __device__ __forceinline__ void row_bits_b(const uint32_t* img, int off, int len, uint64_t (&w)[NW]) {
@@ -963,19 +849,12 @@ __device__ __forceinline__ void row_bits_b(const uint32_t* img, int off, int len
 // readers run past its end)
 __host__ __device__ inline size_t triage_img_bytes(int64_t len) {
     const int64_t nch = (len + 15) / 16 + 2;
-#if QDEC_TRIAGE_BITS
     return (size_t)((2 * (nch + 8) + 15) / 16 * 16);
-#else
-    return (size_t)(16 * nch);
-#endif
 }
 
 // One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).
-#ifndef QDEC_TRIAGE_OCC
-#define QDEC_TRIAGE_OCC 1  // waves per SIMD the triage's registers are budgeted for (A/B)
-#endif
 template <int RC, int NWD>
-__global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
+__global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
     using Ent = CmpEntry<RC>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -998,8 +877,8 @@ __global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph
     const int nlz = want_fail ? g.k * g.lz_words : 0;
     unsigned char* syn_img = smem + ((size_t)nlz * 8 + 15) / 16 * 16;
     unsigned char* rd_img = syn_img + triage_img_bytes(64 * (int64_t)m);
-    // iteration-1 words: past the images (bit images), over them (byte images)
-    unsigned char* it1_base = QDEC_TRIAGE_BITS ? rd_img + triage_img_bytes(64 * (int64_t)nd) : syn_img;
+    // iteration-1 words: past the images
+    unsigned char* it1_base = rd_img + triage_img_bytes(64 * (int64_t)nd);
     for (int e = lane; e < nlz; e += 64) lz_lds[e] = g.lz[e];
     // iteration-1 tables (TriageIt1), loaded ahead of the tiles
     uint64_t it_ids[NWD], it_cv[RC][2];
@@ -1019,32 +898,19 @@ __global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph
     const TileSrc ts(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img);
     const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
                      want_fail ? (int64_t)ns * nd : 0, rd_img);
-#if QDEC_TRIAGE_PAIR
     if (want_fail)
-        tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < QDEC_TRIAGE_UB ? 4 * NWD : QDEC_TRIAGE_UB)>(ts, tr, lane);
+        tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < kTriageUB ? 4 * NWD : kTriageUB)>(ts, tr, lane);
     else tile_to_lds<8>(ts, lane);
-#else
-    tile_to_lds<8>(ts, lane);
-    if (want_fail) tile_to_lds<8>(tr, lane);
-#endif
     __syncthreads();
     const int ssh = ts.shift, rsh = tr.shift;
     const bool live = lane < ns;
     const int64_t shot = s0 + lane;
     uint64_t sw[RC];
-#if QDEC_TRIAGE_BITS
     row_bits_b<RC>(reinterpret_cast<const uint32_t*>(syn_img), ssh + lane * m, m, sw);
-#else
-    row_bits<RC>(reinterpret_cast<const uint32_t*>(syn_img), ssh + lane * m, m, sw);
-#endif
     uint64_t rp[kMaxLogicalRounds] = {0ull, 0ull, 0ull, 0ull};
     if (want_fail) {
         uint64_t rw[NWD];
-#if QDEC_TRIAGE_BITS
         row_bits_b<NWD>(reinterpret_cast<const uint32_t*>(rd_img), rsh + lane * nd, nd, rw);
-#else
-        row_bits<NWD>(reinterpret_cast<const uint32_t*>(rd_img), rsh + lane * nd, nd, rw);
-#endif
         for (int r = 0; r < g.k; ++r) {  // uniform rows of the dense logical table (LDS broadcasts)
             int par = 0;
 #pragma unroll
@@ -1062,9 +928,8 @@ __global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph
     int wt = 0;
 #pragma unroll
     for (int rc = 0; rc < RC; ++rc) wt += __popcll(sw[rc]);
-    const bool it1 = a.it1_lut && __popcll(__ballot(live && wt <= QDEC_T1_GATE_W)) >= QDEC_T1_GATE_N;
+    const bool it1 = a.it1_lut && __popcll(__ballot(live && wt <= kT1GateW)) >= kT1GateN;
     if (it1) {  // uniform: iteration 1 here (TriageIt1)
-        // (byte images: in their place, dead once the rows are bit words)
         wave_lds_sync();
         uint64_t* synT = reinterpret_cast<uint64_t*>(it1_base);
         uint64_t* xT = synT + RC * 64 + 1;
@@ -1072,16 +937,7 @@ __global__ __launch_bounds__(64, QDEC_TRIAGE_OCC) void ms_triage_kernel(DevGraph
         // transpose: lane t gets the word of check rc * 64 + t
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) {
-#if QDEC_T1_BALLOT
-            uint64_t mine = 0ull;
-#pragma unroll
-            for (int t = 0; t < 64; ++t) {
-                const uint64_t wd = __ballot(live && ((sw[rc] >> t) & 1ull));
-                mine = lane == t ? wd : mine;
-            }
-#else
             const uint64_t mine = wave_transpose64(live ? sw[rc] : 0ull, lane);
-#endif
             synT[rc * 64 + lane] = mine;  // checks >= m: zero words
         }
         if (lane == 0) {
@@ -1199,10 +1055,7 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
 
     const int lane = threadIdx.x;
     const int m = g.m;
-#ifndef QDEC_CMP_PIN2
-#define QDEC_CMP_PIN2 1
-#endif
-    if constexpr (QDEC_CMP_PIN2 && sizeof(T) == 8 && OCC == 0) {
+    if constexpr (sizeof(T) == 8 && OCC == 0) {
         // f64 at 2 waves per SIMD (the one-pass kernel's placement): the kernel
         // needs ~160 VGPRs, which would let a CU put 3 waves on one SIMD and 1 on
         // another; claiming v175 makes the allocation 176, so at most 2 per SIMD

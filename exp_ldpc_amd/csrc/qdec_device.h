@@ -386,29 +386,19 @@ __device__ __forceinline__ int lz_row_parity(const DevGraph& g, const uint64_t* 
     return par & 1;
 }
 
-#ifndef QDEC_DEFER_STORES
-#define QDEC_DEFER_STORES 0
-#endif
-#ifndef QDEC_STAGE_DEPTH
-#define QDEC_STAGE_DEPTH 1
-#endif
 template <int RC, int NW>
 struct ShotIo {
     static constexpr int NS = (64 * RC + 3 + 255) / 256;  // syndrome glds per stage
     static constexpr int NR = (64 * NW + 3 + 255) / 256;  // readout glds per stage
     static constexpr int kStaged = NS + NR;
-    // shots staged ahead (QDEC_STAGE_DEPTH): the syndrome of shot k+D is staged
-    // when shot k starts, so a short shot (a zero syndrome at low p) waits for
-    // HBM once per D shots; D syndrome and D + 1 readout buffers
-    static constexpr int kDepth = QDEC_STAGE_DEPTH;
-    static_assert(kDepth == 1 || kDepth == 2, "stage depth");
-    static constexpr int kSynBufs = kDepth, kRdBufs = kDepth + 1;
-    // vmcnt at the loop top (this shot's syndrome landed: its readout loads and
-    // the D - 1 later stages are younger) and before the readout is read (the D
-    // later stages are younger); stores and counter atomics in between only
-    // make either wait stricter
-    static constexpr int kWaitSyn = NR + (kDepth - 1) * kStaged;
-    static constexpr int kWaitRd = kDepth * kStaged;
+    // one shot staged ahead: one syndrome and two readout buffers
+    static constexpr int kSynBufs = 1, kRdBufs = 2;
+    // vmcnt at the loop top (this shot's syndrome landed: its readout loads are
+    // younger) and before the readout is read (the next shot's stage is
+    // younger); stores and counter atomics in between only make either wait
+    // stricter
+    static constexpr int kWaitSyn = NR;
+    static constexpr int kWaitRd = kStaged;
     __host__ __device__ static size_t bytes(const DevGraph& g) {
         size_t b = 256 * (size_t)(NS * kSynBufs + NR * kRdBufs);
         if (lz_in_lds(g)) b += ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16;
@@ -451,12 +441,10 @@ struct ShotIo {
         const int64_t dw0 = start >> 2;
         const uint8_t* base = buf + 4 * dw0;
         int64_t lim64 = total_dw - 1 - dw0;  // last loadable dword, relative (>= 0)
-#ifndef QDEC_STAGE_BUFFER_CLAMP
         // lanes past the row re-read the row's last dword (same line, coalesced
         // in the instruction) instead of fetching the following rows' bytes
         const int64_t row_last = ((start + len - 1) >> 2) - dw0;
         lim64 = row_last < lim64 ? row_last : lim64;
-#endif
         const int lim = lim64 > 0x3fffffff ? 0x3fffffff : (int)lim64;
 #pragma unroll
         for (int c = 0; c < N; ++c) {

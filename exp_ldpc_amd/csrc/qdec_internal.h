@@ -217,8 +217,9 @@ struct DecodeArgs {
     // listing steps (QDEC_SSF_NOSPLIT=1; parity tests run both ways)
     int ssf_nosplit;
     // optional timing (host side only): events recorded on the launch stream
-    // before the BP kernel, after it, and after the SSF kernel
-    hipEvent_t* ev;    // [3] or nullptr
+    // before the BP kernel, after it, after the SSF kernel, and after the BP
+    // stage's pre-pass (record_ev)
+    hipEvent_t* ev;    // [4] or nullptr
     // compact shot list of lean min-sum wave launches (ms_triage_kernel ->
     // bp_ms_cmp_kernel), in kCmpSegs segments: triage tile t appends to
     // segment t % kCmpSegs, whose entries [cmp_cap][CmpEntry::EW] u64 start at
@@ -255,8 +256,12 @@ struct OsdArgs {
 bool osd_kernel_supports(const DevGraph& g);
 int launch_osd(const DevGraph& g, const OsdArgs& a, int num_cus, hipStream_t stream);
 
+// ev[3] marks the end of a pre-pass inside the BP timing (the shot triage):
+// recorded with ev[0] and again after the pre-pass when one runs
 inline void record_ev(const DecodeArgs& a, int i, hipStream_t s) {
-    if (a.ev) (void)hipEventRecord(a.ev[i], s);
+    if (!a.ev) return;
+    (void)hipEventRecord(a.ev[i], s);
+    if (i == 0) (void)hipEventRecord(a.ev[3], s);
 }
 
 // Names of the BP and SSF kernels the calling host thread's last launch_decode

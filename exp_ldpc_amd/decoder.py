@@ -315,6 +315,21 @@ class Decoder:
                    "qd_graph_read_timing")
         return bp[:cnt.value].astype(np.float64), ssf[:cnt.value].astype(np.float64)
 
+    def read_timing_detail(self):
+        """(pre_ms, bp_ms, ssf_ms, listed) per recorded call: the BP stage's
+        pre-pass (shot triage), the BP kernel alone, the SSF kernel, and the
+        shots the triage left to the BP kernel (-1: no two-pass launch);
+        resets the ring."""
+        cap = getattr(self, "_t_cap", 0)
+        pre, bp, ssf = (np.zeros(max(cap, 1), np.float32) for _ in range(3))
+        listed = np.zeros(max(cap, 1), np.int64)
+        cnt = C.c_int32(0)
+        _abi.check(self._lib.qd_graph_read_timing_detail(self._handle, _abi.ptr(pre), _abi.ptr(bp), _abi.ptr(ssf),
+                                                         _abi.ptr(listed), cap, C.byref(cnt)),
+                   "qd_graph_read_timing_detail")
+        n = cnt.value
+        return pre[:n].astype(np.float64), bp[:n].astype(np.float64), ssf[:n].astype(np.float64), listed[:n]
+
     def last_kernels(self) -> tuple[str, str, str]:
         """(BP kernel, SSF kernel, pre-pass) the last decode call launched, in
         rocprofv3's spelling with template arguments ("" for a stage that did

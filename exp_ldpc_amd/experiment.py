@@ -148,6 +148,11 @@ class BatchPipeline:
         """The BP decoders this pipeline launches (for the timing ring)."""
         return [d for d in (getattr(self, k, None) for k in ("st", "fin", "ss", "det")) if d is not None]
 
+    def launches_per_batch(self, dec) -> int:
+        """Decode calls `dec` receives per run(): the single-shot decoder runs
+        once per syndrome round, every other decoder once."""
+        return self.R if dec is getattr(self, "ss", None) else 1
+
     def _fail_host(self, readout, corr):
         if self.L.shape[0] == 0:
             return np.zeros(readout.shape[0], bool)
@@ -497,15 +502,27 @@ class ShardError(RuntimeError):
         self.p_ph, self.device, self.lo, self.hi, self.cause = p_ph, device, lo, hi, cause
 
 
+def device_error(e: BaseException) -> bool:
+    """True for failures of the device itself (a HIP error from the library --
+    codes <= -100, a failed launch or allocation -- or from torch): a retry on
+    the same device would only meet the same sticky error."""
+    from ._abi import QdecError
+    if isinstance(e, QdecError):
+        return getattr(e, "rc", 0) <= -100
+    msg = str(e)
+    return isinstance(e, RuntimeError) and ("HIP error" in msg or "hipError" in msg)
+
+
 def run_shards(shards, work, p_ph=None, retries: int = 1):
     """Run work(device, lo, hi, attempt) -> counters for every (device, lo, hi)
     shard, one host thread per shard (each blocks on its own device's copies),
-    and sum the counters.  A shard that raises is run again in a fresh worker
-    thread on the same device (its handles rebuilt by `work` when attempt > 0;
-    never a re-exec of a process that touched the GPU), up to `retries` times;
-    then ShardError names the point and the failed shot range.  The reference
-    fan-out (misc/p_sweep.py:24-40, Pool.starmap) aborts the sweep on any
-    worker exception."""
+    and sum the counters.  A shard that raises a host-side exception is run
+    again in a fresh worker thread on the same device (its handles rebuilt by
+    `work` when attempt > 0; never a re-exec of a process that touched the GPU),
+    up to `retries` times; then ShardError names the point and the failed shot
+    range.  A device error (device_error) is not retried: ShardError at once.
+    The reference fan-out (misc/p_sweep.py:24-40, Pool.starmap) aborts the sweep
+    on any worker exception."""
     from concurrent.futures import ThreadPoolExecutor
 
     def attempt(i, k):
@@ -532,8 +549,9 @@ def run_shards(shards, work, p_ph=None, retries: int = 1):
         if not errors:
             break
         pending = sorted(errors)
-        if k == retries:
+        if k == retries or any(device_error(e) for e in errors.values()):
             i = pending[0]
+            i = next((j for j in pending if device_error(errors[j])), i)
             d, lo, hi = shards[i]
             raise ShardError(p_ph, d, lo, hi, errors[i]) from errors[i]
     n = max(len(r) for r in results)
@@ -603,11 +621,15 @@ def p_sweep(samples, p_values, noise_model, noise_model_args, meas_prior, data_p
             """Shard i's contiguous shot range on device devs[i]; returns its
             counters (failures, converged, iterations, SSF steps, kernel ms)."""
             d = devs[i]
-            pipe = pipes[i] if attempt == 0 else pipeline(d)  # a retry rebuilds its handles
+            if attempt > 0:  # a retry frees the failed pipeline's handles, then rebuilds them
+                for dec in pipes[i].decoders() + [pipes[i].sampler_graph]:
+                    dec.close()
+                pipes[i] = pipeline(d)
+            pipe = pipes[i]
             nb = max(1, -(-(hi - lo) // batch))
             decs = pipe.decoders()
-            for dec in decs:
-                dec.set_timing(nb)
+            for dec in decs:  # one ring slot per decode call (ss: one per round)
+                dec.set_timing(nb * pipe.launches_per_batch(dec))
             acc = [0, 0, 0, 0, 0.0]
             with torch.cuda.device(d):
                 for start in range(lo, hi, batch):

@@ -17,7 +17,7 @@ equals a single-process run over the same range.
 from __future__ import annotations
 
 __all__ = ["BOOKKEEPING_BACKEND", "init_process_group", "rank_device", "step_shot0", "shard_range",
-           "reduce_counts", "max_time", "barrier"]
+           "reduce_counts", "max_time", "barrier", "gather_rows"]
 
 # the backend of the bookkeeping group: host tensors only (see the module doc)
 BOOKKEEPING_BACKEND = "gloo"
@@ -104,6 +104,20 @@ def max_time(seconds: float) -> float:
     t = torch.tensor([float(seconds)], dtype=torch.float64)
     d.all_reduce(t, op=d.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_rows(values) -> list:
+    """Every rank's row of floats, in rank order (one all_gather of host words;
+    [values] when not distributed): per-rank timings and device ordinals for
+    rank 0's report."""
+    import torch
+    t = _host(values, torch.float64).clone().reshape(-1)
+    d = _dist()
+    if d is None or d.get_world_size() == 1:
+        return [t.tolist()]
+    out = [torch.zeros_like(t) for _ in range(d.get_world_size())]
+    d.all_gather(out, t)
+    return [o.tolist() for o in out]
 
 
 def barrier() -> None:

@@ -201,6 +201,14 @@ int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
  * only 2).  Results are identical at every setting.  No reference counterpart. */
 int qd_graph_set_wave_occupancy(qd_graph* g, int32_t waves_per_cu);
 int qd_graph_read_timing(qd_graph* g, float* bp_ms, float* ssf_ms, int32_t max_calls, int32_t* n_calls);
+/* The same ring split finer: per recorded call the BP stage's pre-pass (the
+ * lean launches' shot triage; 0 when none ran), the BP kernel alone, the SSF
+ * kernel (ms), and `listed` = the number of shots the triage left to the BP
+ * kernel (-1 when the call did not run the two-pass path).  Resets the ring
+ * like qd_graph_read_timing.  Any output may be NULL.  No reference
+ * counterpart. */
+int qd_graph_read_timing_detail(qd_graph* g, float* pre_ms, float* bp_ms, float* ssf_ms, int64_t* listed,
+                                int32_t max_calls, int32_t* n_calls);
 
 /* Names of the BP and SSF kernels the last decode call on `g` launched, and of
  * the pass run before the BP kernel inside the BP timing (the lean launches'

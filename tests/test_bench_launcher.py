@@ -30,3 +30,8 @@ def test_bench_gpus2_self_launches_two_ranks_and_merges():
         assert row["shots"] == 4000
         assert row["failures"] == 2000
     assert r["value"] > 0 and r["ms_per_step"] > 0
+    # per-rank record: every rank seen once, its own timing and shot count
+    assert r["ranks_seen"] == 2 and [x["rank"] for x in r["ranks"]] == [0, 1]
+    for x in r["ranks"]:
+        assert x["device"] == -1 and x["shots"] == 2 * 1000 * 3 and x["timed_s"] > 0
+    assert max(x["timed_s"] for x in r["ranks"]) <= r["ms_per_step"] * r["steps"] / 1e3 * 1.0001

@@ -244,6 +244,27 @@ def test_run_shards_reports_the_failed_range():
     assert run_shards([(0, 0, 7)], once) == [7] and seen == [0, 1]
 
 
+def test_run_shards_does_not_retry_device_errors():
+    """A HIP error (library status <= -100, or torch's HIP RuntimeError) is
+    sticky on its device: no retry, ShardError at once naming that shard."""
+    from exp_ldpc_amd._abi import QdecError
+    from exp_ldpc_amd.experiment import ShardError, device_error, run_shards
+    assert device_error(QdecError("decode launch failed", -101)) and not device_error(QdecError("bad arg", -7))
+    assert device_error(RuntimeError("HIP error: an illegal memory access")) and not device_error(ValueError("x"))
+    for exc in (QdecError("qd_decode_batch_device failed (-101)", -101), RuntimeError("HIP error: launch failure")):
+        seen = []
+
+        def work(d, lo, hi, attempt, exc=exc):
+            seen.append((lo, attempt))
+            if lo == 5:
+                raise exc
+            return [1]
+
+        with pytest.raises(ShardError) as ei:
+            run_shards([(0, 0, 5), (1, 5, 9)], work, p_ph=0.03)
+        assert (ei.value.device, ei.value.lo) == (1, 5) and all(a == 0 for _, a in seen)
+
+
 def test_set_logicals_rejects_1d_dense_input():
     """A 1-D dense logicals argument is malformed (k x n_data expected); it must
     not be read as a single logical row.  Checked before any device call."""
