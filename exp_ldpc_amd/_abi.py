@@ -84,6 +84,8 @@ SIGNATURES = {
     "qd_graph_get_option": (_i32, [_p, _i32, C.POINTER(_i32)]),
     "qd_graph_ssf_tables": (_i32, [_p, C.POINTER(_i32), C.POINTER(_i64)]),
     "qd_graph_ssf_tables_copy": (_i32, [_p, _p, _p, _p, _p, C.POINTER(_i32), C.POINTER(_i32)]),
+    "qd_graph_queue_layout": (_i32, [_p, _i64, _p]),
+    "qd_graph_it1_tables_copy": (_i32, [_p, _i32, _p, _p, C.POINTER(_i32)]),
     "qd_gf2_rref": (_i64, [_p, _i64, _i64, _i64, _p, _i32]),
     "qd_gf2_extend_basis": (_i64, [_p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64]),
 }

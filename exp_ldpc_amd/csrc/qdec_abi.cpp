@@ -742,6 +742,32 @@ void build_tables(qd_graph* G, int m, int n) {
 // syndrome words, readout logical-parity words.
 size_t cmp_entry_bytes(const DevGraph& g) { return 8 * (1 + (size_t)g.m_pad / 64 + 4); }
 
+// Byte layout of the queue scratch for a capacity of `cap` shots: the queue
+// count (256 B), idx[cap] u64, then the byte-format x[cap][n] | r[cap][m] region
+// (the packed format of the wave kernels reuses it for [cap][1 + 2 n_pad/64 +
+// m_pad/64] u64 entries), and for wave graphs the compact shot list:
+// kCmpSegs counters on their own 128-B lines (the triage's u64 atomics need
+// natural alignment, so the region starts on a 256-B boundary), then the
+// segments of cmp_seg_cap(cap) entries.
+struct QueueLayout {
+    size_t bytes, idx, x, r, cmp_count, cmp;
+    int64_t cmp_cap;
+};
+QueueLayout queue_layout(const DevGraph& g, int64_t cap) {
+    QueueLayout L{};
+    const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
+    const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
+    L.idx = 256;
+    L.x = 256 + (size_t)cap * 8;
+    L.r = L.x + (size_t)cap * g.n;
+    const size_t cbase = 256 + ((size_t)cap * (8 + xr) + 255) / 256 * 256 + 256;
+    L.cmp_count = g.wave ? cbase : 0;
+    L.cmp = g.wave ? cbase + (size_t)kCmpSegs * 128 : 0;
+    L.cmp_cap = g.wave ? cmp_seg_cap(cap) : 0;
+    L.bytes = cbase + (g.wave ? (size_t)kCmpSegs * 128 + (size_t)kCmpSegs * L.cmp_cap * cmp_entry_bytes(g) : 0) + 256;
+    return L;
+}
+
 // Attach the SSF queue scratch (capacity >= B shots) and, for wave graphs, the
 // compact shot list of lean launches to the launch arguments.
 void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
@@ -754,33 +780,20 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
         if (G->qws) hip_check(hipFree(G->qws), "hipFree queue");
         G->qws = nullptr;
         G->q_cap = 0;
-        // byte format: idx[B] | x[B][n] | r[B][m]; packed format (wave kernels) reuses
-        // the x region for [B][1 + 2 n_pad/64 + m_pad/64] u64 entries; then the
-        // compact list [B] entries (wave graphs)
-        const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
-        const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
-        const size_t cl = g.wave ? cmp_entry_bytes(g) : 0;
-        const size_t cmp_bytes = g.wave ? (size_t)kCmpSegs * 128 + (size_t)kCmpSegs * cmp_seg_cap(a.B) * cl : 0;
-        const size_t bytes = 256 + ((size_t)a.B * (8 + xr) + 255) / 256 * 256 + 256 + cmp_bytes + 256;
-        hip_check(hipMalloc(&G->qws, bytes), "hipMalloc queue");
+        hip_check(hipMalloc(&G->qws, queue_layout(g, a.B).bytes), "hipMalloc queue");
         G->q_cap = a.B;
     }
+    const QueueLayout L = queue_layout(g, G->q_cap);
     auto* base = static_cast<uint8_t*>(G->qws);
     a.q_count = reinterpret_cast<int32_t*>(base);
-    a.q_idx = reinterpret_cast<int64_t*>(base + 256);
-    a.q_x = base + 256 + (size_t)G->q_cap * 8;
-    a.q_r = a.q_x + (size_t)G->q_cap * g.n;
+    a.q_idx = reinterpret_cast<int64_t*>(base + L.idx);
+    a.q_x = base + L.x;
+    a.q_r = base + L.r;
     a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
     if (g.wave) {
-        const size_t packed = 8 * (1 + 2 * (size_t)g.n_pad / 64 + (size_t)g.m_pad / 64);
-        const size_t xr = std::max((size_t)g.n + (size_t)g.m, packed);
-        // kCmpSegs counters (one 128-B line each: the triage's u64 atomics need
-        // natural alignment, so the region starts on a 256-B boundary), then
-        // the segments
-        uint8_t* cbase = base + 256 + ((size_t)G->q_cap * (8 + xr) + 255) / 256 * 256 + 256;
-        a.cmp_count = reinterpret_cast<unsigned long long*>(cbase);
-        a.cmp = reinterpret_cast<uint64_t*>(cbase + (size_t)kCmpSegs * 128);
-        a.cmp_cap = cmp_seg_cap(G->q_cap);
+        a.cmp_count = reinterpret_cast<unsigned long long*>(base + L.cmp_count);
+        a.cmp = reinterpret_cast<uint64_t*>(base + L.cmp);
+        a.cmp_cap = L.cmp_cap;
     }
 }
 
@@ -1744,6 +1757,30 @@ int qd_graph_ssf_tables_copy(const qd_graph* G, uint32_t* lut, uint32_t* off, ui
         put(off, g.s_off, (size_t)g.g_pad);
         put(lcw, g.s_lcw, (size_t)kLutLCW * g.g_pad);
         put(tog, g.s_tog, (size_t)g.m_pad * 64);
+    });
+}
+
+int qd_graph_queue_layout(const qd_graph* G, int64_t B, int64_t* out) {
+    return guarded([&] {
+        check_graph(G);
+        if (B <= 0 || !out) throw Fail(-8, "invalid batch or null output");
+        const QueueLayout L = queue_layout(G->dg, B);
+        const int64_t v[8] = {(int64_t)L.bytes, (int64_t)L.idx, (int64_t)L.x, (int64_t)L.r, (int64_t)L.cmp_count,
+                              (int64_t)L.cmp, L.cmp_cap, (int64_t)cmp_entry_bytes(G->dg)};
+        std::memcpy(out, v, sizeof(v));
+    });
+}
+
+int qd_graph_it1_tables_copy(const qd_graph* G, int32_t precision, uint16_t* lut, uint64_t* vchk, int32_t* n_pad) {
+    return guarded([&] {
+        check_graph(G);
+        if (!G->host_only) throw Fail(-16, "table copies are kept for host-only graphs (qd_graph_create_host)");
+        if (precision != QD_F64 && precision != QD_F32) throw Fail(-4, "invalid precision");
+        const DevGraph& g = G->dg;
+        if (n_pad) *n_pad = g.n_pad;
+        if (!g.it1_lut[precision] || !g.it1_vchk) throw Fail(-37, "no iteration-1 tables for this precision");
+        if (lut) std::memcpy(lut, g.it1_lut[precision], (size_t)g.n_pad * 2);
+        if (vchk) std::memcpy(vchk, g.it1_vchk, (size_t)g.n_pad * 8);
     });
 }
 

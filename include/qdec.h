@@ -268,6 +268,21 @@ int qd_graph_ssf_tables(const qd_graph* g, int32_t* has_lut, int64_t* lut_bytes)
  * [lut_bytes / 4], off [g_pad], lcw [4][g_pad], tog [m_pad][64] (u32 each; the
  * layouts of DevGraph::s_lut / s_off / s_lcw / s_tog in qdec_internal.h);
  * *g_pad and *m_pad receive the strides.  Any output may be NULL. */
+/* Host-side layout of the handle's queue scratch for a batch of B shots (the
+ * workspace attach_queue allocates; tests check its alignment and capacities
+ * on host-only graphs): out[8] = total bytes, offsets of the shot-index array,
+ * the hard-decision / packed-entry region, the residual region, the compact
+ * list's 64 segment counters and its entries, the entries per segment, the
+ * bytes per entry.  No reference counterpart. */
+int qd_graph_queue_layout(const qd_graph* g, int64_t B, int64_t* out);
+
+/* Copies of the triage's iteration-1 tables (host-only graphs): lut[n_pad]
+ * (bit b = column j's hard decision after min-sum iteration 1 under syndrome
+ * pattern b of its checks, in the kernels' precision and summation order) and
+ * vchk[n_pad] (the checks of column j's edges, 4 x u16, pad = m).  Fails when
+ * the precision has no tables (a prior <= 0).  No reference counterpart. */
+int qd_graph_it1_tables_copy(const qd_graph* g, int32_t precision, uint16_t* lut, uint64_t* vchk, int32_t* n_pad);
+
 int qd_graph_ssf_tables_copy(const qd_graph* g, uint32_t* lut, uint32_t* off, uint32_t* lcw, uint32_t* tog,
                              int32_t* g_pad, int32_t* m_pad);
 

@@ -435,3 +435,72 @@ def test_ssf_lut_tables_follow_the_spec(code225, oracle_lib, max_steps):
         assert checked > 100 and ref["ssf_steps"].sum() > 200
     finally:
         lib.qd_graph_destroy(h)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_host_only_it1_tables_equal_the_oracle_iteration_1(code225, oracle_lib, precision):
+    """The triage's iteration-1 tables (it1_tables, qdec_abi.cpp), built by a
+    host-only graph: for random per-column priors (with exact ties) and random
+    syndromes, looking up each column's decision under its checks' syndrome
+    pattern equals the oracle's hard decision after min-sum iteration 1
+    (ldpc v1 restatement, max_iter = 1).  A non-positive prior builds no
+    table for the precision.  tools/sanitize.sh runs this under ASan + UBSan."""
+    import ctypes as C
+
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    hz = sp.csr_matrix(code225.checks.z)
+    m, n = hz.shape
+    rng = np.random.default_rng(3)
+    probs = rng.choice([0.001, 0.01, 0.02, 0.05, 0.1], size=n)  # ties inside rows
+    h, _, _ = _host_graph(lib, hz, probs=probs)
+    try:
+        prec = _abi.QD_F64 if precision == "f64" else _abi.QD_F32
+        npad = C.c_int32(0)
+        _abi.check(lib.qd_graph_it1_tables_copy(h, prec, None, None, C.byref(npad)), "it1 copy")
+        lut = np.zeros(npad.value, np.uint16)
+        vchk = np.zeros(npad.value, np.uint64)
+        _abi.check(lib.qd_graph_it1_tables_copy(h, prec, _abi.ptr(lut), _abi.ptr(vchk), None), "it1 copy")
+        B = 400
+        syn = (rng.random((B, m)) < 0.08).astype(np.uint8)
+        ref = oracle_lib.decode(hz, probs, syn, method="ms", precision=precision, max_iter=1, want_llr=False)
+        synp = np.concatenate([syn, np.zeros((B, 1), np.uint8)], axis=1)  # pad check id m -> 0
+        ids = np.stack([((vchk[:n] >> np.uint64(16 * k)) & np.uint64(0xffff)).astype(np.int64) for k in range(4)], 1)
+        pat = sum(synp[:, ids[:, k]].astype(np.int64) << k for k in range(4))
+        got = ((lut[:n].astype(np.int64)[None, :] >> pat) & 1).astype(np.uint8)
+        assert np.array_equal(got, ref["x"])
+    finally:
+        lib.qd_graph_destroy(h)
+    h2, _, _ = _host_graph(lib, hz, probs=np.where(np.arange(n) == 7, 0.6, 0.01))  # a negative LLR
+    try:
+        assert lib.qd_graph_it1_tables_copy(h2, _abi.QD_F64, None, None, None) != 0
+    finally:
+        lib.qd_graph_destroy(h2)
+
+
+def test_host_only_queue_layout(code225):
+    """The queue scratch layout attach_queue allocates (queue_layout,
+    qdec_abi.cpp), computed on a host-only graph for batches around the
+    64-shot tile and segment sizes: regions in order and disjoint, the compact
+    list's counters on a 256-B boundary (u64 atomics) and its entry region
+    16-B aligned, and enough segment capacity for every
+    shot of every tile (tile t -> segment t mod 64)."""
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    hz = code225.checks.z
+    h, _, _ = _host_graph(lib, hz, gens=code225.checks.x, probs=0.01)
+    try:
+        m, n = hz.shape
+        for B in (1, 63, 64, 65, 4095, 4097, 64 * 64 + 1, 1 << 18, (1 << 18) + 13):
+            out = np.zeros(8, np.int64)
+            _abi.check(lib.qd_graph_queue_layout(h, B, _abi.ptr(out)), "layout")
+            total, idx, x, r, cnt, cmp, cap, ent = (int(v) for v in out)
+            assert idx == 256 and x == idx + 8 * B and r == x + B * n
+            packed = 8 * (1 + 2 * 256 // 64 + 128 // 64)
+            assert cnt >= x + B * max(n + m, packed) and cnt % 256 == 0
+            assert cmp == cnt + 64 * 128 and cmp % 16 == 0 and ent % 16 == 8 and ent == 8 * (1 + 2 + 4)
+            tiles = -(-B // 64)
+            assert cap * 64 >= B and cap >= 64 * (-(-tiles // 64)) and cap % 64 == 0
+            assert total >= cmp + 64 * cap * ent
+    finally:
+        lib.qd_graph_destroy(h)
