@@ -309,7 +309,7 @@ def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
     return res
 
 
-def c4_line(dev, shots: int = 1 << 17, ps=(0.01, 0.03), precisions=("f64", "f32")):
+def c4_line(dev, shots: int = 1 << 17, ps=(0.005, 0.01, 0.03), precisions=("f64", "f32")):
     """BASELINE config 4's code on one GPU (the driver's record of it; the
     config itself shards 1e7 shots over 8 GPUs exactly as the headline does):
     biregular_hgp(80, 3, 4, seed=2025), n = 10^4 (reference-generated checks,

@@ -106,7 +106,7 @@ struct qd_graph {
     int t_cap = 0, t_count = 0;
     // per timed call: compact-list length of a two-pass launch (summed segment
     // counters, copied into pinned memory behind the launch), -1 otherwise
-    uint64_t* t_listed = nullptr;  // [t_cap][kCmpSegs], hipHostMalloc
+    uint64_t* t_listed = nullptr;  // [t_cap][kCmpLists * kCmpSegs], hipHostMalloc
     std::vector<int> t_cmp;
     // min-sum wave kernel: variable (column) held by each lane slot, -1 for pads
     std::vector<int> ms_var_of_slot;
@@ -762,9 +762,10 @@ QueueLayout queue_layout(const DevGraph& g, int64_t cap) {
     L.r = L.x + (size_t)cap * g.n;
     const size_t cbase = 256 + ((size_t)cap * (8 + xr) + 255) / 256 * 256 + 256;
     L.cmp_count = g.wave ? cbase : 0;
-    L.cmp = g.wave ? cbase + (size_t)kCmpSegs * 128 : 0;
+    L.cmp = g.wave ? cbase + (size_t)kCmpLists * kCmpSegs * 128 : 0;
     L.cmp_cap = g.wave ? cmp_seg_cap(cap) : 0;
-    L.bytes = cbase + (g.wave ? (size_t)kCmpSegs * 128 + (size_t)kCmpSegs * L.cmp_cap * cmp_entry_bytes(g) : 0) + 256;
+    L.bytes = cbase +
+              (g.wave ? (size_t)kCmpLists * kCmpSegs * (128 + (size_t)L.cmp_cap * cmp_entry_bytes(g)) : 0) + 256;
     return L;
 }
 
@@ -852,7 +853,8 @@ void note_listed(qd_graph* G, const DecodeArgs& a, hipStream_t s) {
     const bool cmp = !G->last_pre.empty() && a.cmp_count;
     G->t_cmp[slot] = cmp ? 1 : 0;
     if (cmp)
-        hip_check(hipMemcpy2DAsync(G->t_listed + slot * kCmpSegs, 8, a.cmp_count, 128, 8, kCmpSegs,
+        hip_check(hipMemcpy2DAsync(G->t_listed + slot * kCmpLists * kCmpSegs, 8, a.cmp_count, 128, 8,
+                                   kCmpLists * kCmpSegs,
                                    hipMemcpyDeviceToHost, s),
                   "hipMemcpy2DAsync list counters");
 }
@@ -1084,7 +1086,7 @@ static void ssf_lut_tables(qd_graph* G, int n_gen, const int32_t* gen_ptr, const
     std::vector<int> shape_off;
     std::vector<uint32_t> off(gp, 0);
     std::vector<uint32_t> lcw((size_t)kLutLCW * gp, 0xffffffffu);
-    std::vector<uint32_t> tog((size_t)g.m_pad * 64, 0);
+    std::vector<uint32_t> tog(((size_t)g.m_pad + 1) * 64, 0);  // row m_pad: zero (the kernel's unflipped bits)
     int total = 0;
     for (int gi = 0; gi < n_gen; ++gi) {
         const int a = gen_ptr[gi], w = gen_ptr[gi + 1] - a;
@@ -1128,7 +1130,7 @@ static void ssf_lut_tables(qd_graph* G, int n_gen, const int32_t* gen_ptr, const
             tog[(size_t)c * 64 + (gi & 63)] |= (1u << b) << (16 * (gi >> 6));
         }
     }
-    if ((size_t)total * 4 + (size_t)g.m_pad * 256 > kLutBudget) return;
+    if ((size_t)total * 4 + ((size_t)g.m_pad + 1) * 256 > kLutBudget) return;
     // best (score, t) of every local syndrome of every shape; scores -> ranks
     std::vector<int> score(total, 0);
     std::vector<uint32_t> lut(total, 0);
@@ -1616,7 +1618,8 @@ int qd_graph_set_timing(qd_graph* G, int32_t capacity) {
         for (auto& e : G->tev) hip_check(hipEventCreate(&e), "hipEventCreate");
         if (capacity > 0) {
             void* h = nullptr;
-            hip_check(hipHostMalloc(&h, (size_t)capacity * kCmpSegs * 8, hipHostMallocDefault), "hipHostMalloc");
+            hip_check(hipHostMalloc(&h, (size_t)capacity * kCmpLists * kCmpSegs * 8, hipHostMallocDefault),
+                      "hipHostMalloc");
             G->t_listed = static_cast<uint64_t*>(h);
             G->t_cmp.assign(capacity, 0);
         }
@@ -1667,7 +1670,8 @@ int qd_graph_read_timing_detail(qd_graph* G, float* pre_ms, float* bp_ms, float*
                 int64_t c = -1;
                 if (G->t_cmp[i]) {
                     c = 0;
-                    for (int k = 0; k < kCmpSegs; ++k) c += (int64_t)G->t_listed[(size_t)i * kCmpSegs + k];
+                    for (int k = 0; k < kCmpLists * kCmpSegs; ++k)
+                        c += (int64_t)G->t_listed[((size_t)i * kCmpLists) * kCmpSegs + k];
                 }
                 listed[i] = c;
             }
@@ -1756,7 +1760,7 @@ int qd_graph_ssf_tables_copy(const qd_graph* G, uint32_t* lut, uint32_t* off, ui
         put(lut, g.s_lut, (size_t)g.s_lut_n);
         put(off, g.s_off, (size_t)g.g_pad);
         put(lcw, g.s_lcw, (size_t)kLutLCW * g.g_pad);
-        put(tog, g.s_tog, (size_t)g.m_pad * 64);
+        put(tog, g.s_tog, ((size_t)g.m_pad + 1) * 64);
     });
 }
 

@@ -651,7 +651,8 @@ constexpr int kLutOcc = 8;     // waves per SIMD the table-driven kernel is comp
 struct SsfLutLds {
     static constexpr int kStage = 3;  // packed queue entries staged per wave (two slots ahead)
     __host__ __device__ static size_t lut_bytes(const DevGraph& g) { return ((size_t)g.s_lut_n * 4 + 15) / 16 * 16; }
-    __host__ __device__ static size_t tog_bytes(const DevGraph& g) { return (size_t)g.m_pad * 64 * 4; }
+    // toggle rows [m_pad + 1][64] (the last one zero)
+    __host__ __device__ static size_t tog_bytes(const DevGraph& g) { return ((size_t)g.m_pad + 1) * 64 * 4; }
     __host__ __device__ static size_t lz_bytes(const DevGraph& g) {
         return lz_in_lds(g) ? ((size_t)g.k * g.lz_words * 8 + 15) / 16 * 16 : 0;
     }
@@ -659,9 +660,12 @@ struct SsfLutLds {
     __host__ __device__ static size_t shared_bytes(const DevGraph& g) {
         return lut_bytes(g) + tog_bytes(g) + qt_bytes + lz_bytes(g);
     }
-    // staged queue entries, hard decision bytes
+    // staged queue entries, hard decision as bit words (u32 [n_pad / 32]), the
+    // step log (u16 [m_pad]: a shot takes at most m steps), hard decision bytes
+    // (non-lean finalisation)
     __host__ __device__ static size_t wave_bytes(const DevGraph& g) {
-        return 256 * kStage + ((size_t)g.n_pad + 64 + 15) / 16 * 16;
+        return 256 * kStage + (size_t)g.n_pad / 8 + ((size_t)g.m_pad * 2 + 15) / 16 * 16 +
+               ((size_t)g.n_pad + 64 + 15) / 16 * 16;
     }
 };
 
@@ -683,7 +687,9 @@ __global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_ke
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned char* wbase = smem + SsfLutLds::shared_bytes(g) + (size_t)wave * SsfLutLds::wave_bytes(g);
     uint8_t* ent = wbase;                                  // [kStage][256] queue entries
-    uint8_t* xh = wbase + 256 * SsfLutLds::kStage;         // [n_pad + 64] hard decision
+    uint32_t* xb = reinterpret_cast<uint32_t*>(wbase + 256 * SsfLutLds::kStage);  // [n_pad / 32] hard decision bits
+    uint16_t* flog = reinterpret_cast<uint16_t*>(xb + g.n_pad / 32);                 // [m_pad] (g, t) of every step
+    uint8_t* xh = reinterpret_cast<uint8_t*>(flog) + ((size_t)g.m_pad * 2 + 15) / 16 * 16;  // [n_pad + 64] bytes
 
     {   // tables -> LDS, 16-B copies (every size is a multiple of 16 B)
         const uint4* src = reinterpret_cast<const uint4*>(g.s_lut);
@@ -734,8 +740,7 @@ __global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_ke
         wait_vmem<1>();
         const uint64_t* ew = reinterpret_cast<const uint64_t*>(ent + 256 * sb);
         const int64_t shot = (int64_t)ew[0];
-#pragma unroll
-        for (int w = 0; w < XW; ++w) xh[w * 64 + lane] = (uint8_t)((ew[1 + w] >> lane) & 1);
+        if (lane < 2 * XW) xb[lane] = reinterpret_cast<const uint32_t*>(ew + 1)[lane];
         uint64_t R[RW];  // residual words (uniform)
 #pragma unroll
         for (int w = 0; w < RW; ++w) {
@@ -746,7 +751,9 @@ __global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_ke
         wait_lds();
         const int64_t slot2 = seq.next(lane);
         stage_entry((int)min(slot2, (int64_t)count), sb == 0 ? 2 : sb - 1);
-        // first local syndromes: the toggle rows of the violated checks
+        // first local syndromes: the toggle rows of the violated checks, 8 rows
+        // per round (independent LDS reads, one wait; row m_pad is all zero)
+        const uint32_t zrow = (uint32_t)g.m_pad;
         uint32_t sl = 0;
         int sw = 0;
 #pragma unroll
@@ -754,9 +761,17 @@ __global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_ke
             uint64_t bits = R[w];
             sw += __popcll(bits);
             while (bits) {
-                const int c = w * 64 + __builtin_ctzll(bits);
-                bits &= bits - 1;
-                sl ^= tog[c * 64 + lane];
+                uint32_t t = 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    uint32_t c = zrow;
+                    if (bits) {
+                        c = (uint32_t)(w * 64 + __builtin_ctzll(bits));
+                        bits &= bits - 1;
+                    }
+                    t ^= tog[c * 64 + lane];
+                }
+                sl ^= t;
             }
         }
         int steps = 0;
@@ -784,29 +799,49 @@ __global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_ke
             const uint32_t fm = (esel >> 8) & 0xffffu;
             sw -= __builtin_popcount(slg) - __builtin_popcount(slg ^ fm);
             ++steps;
-            // ---- 3. toggle the flipped checks' local-syndrome bits, flip the qubits ----
+            // ---- 3. toggle the flipped checks' local-syndrome bits: one read
+            // of a toggle row per flipped check, each behind a uniform branch and
+            // all issued before the first XOR (one LDS round trip); flip the qubits ----
+            uint32_t tr[kLutLC];
 #pragma unroll
             for (int w = 0; w < kLutLCW; ++w) {
-                uint32_t bits = (fm >> (4 * w)) & 0xfu;
-                if (bits) {
-                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)(hi ? lcw[RG - 1][w] : lcw[0][w]), owner);
-                    do {
-                        const int b = __builtin_ctz(bits);
-                        bits &= bits - 1;
-                        sl ^= tog[((word >> (8 * b)) & 0xffu) * 64 + lane];
-                    } while (bits);
+                const uint32_t nib = (fm >> (4 * w)) & 0xfu;
+                const uint32_t word =
+                    nib ? (uint32_t)__builtin_amdgcn_readlane((int)(hi ? lcw[RG - 1][w] : lcw[0][w]), owner) : 0u;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    tr[4 * w + b] = 0u;
+                    if ((nib >> b) & 1u) tr[4 * w + b] = tog[((word >> (8 * b)) & 0xffu) * 64 + lane];
                 }
             }
-            if (lane < kGenW && ((tsel >> lane) & 1)) {
-                const uint32_t pair = qt[(lane >> 1) * 128 + gsel];
-                xh[(pair >> (16 * (lane & 1))) & 0xffffu] ^= 1;
+            uint32_t tg = 0;
+#pragma unroll
+            for (int b = 0; b < kLutLC; ++b) tg ^= tr[b];
+            sl ^= tg;
+            // the flip itself is logged (steps <= m: every step lowers |s|) and
+            // applied to the hard decision once, after the last step
+            if (lane == 0) flog[steps - 1] = (uint16_t)(gsel | (tsel << 8));
+        }
+        wave_lds_sync();
+        // x ^= 1_F of every logged step: lane s takes step s, its qubits' bits by
+        // LDS atomic XOR (a qubit flipped twice cancels, in any order)
+        for (int b0 = 0; b0 < steps; b0 += 64) {
+            if (b0 + lane < steps) {
+                const uint32_t e = flog[b0 + lane];
+                const int gg = (int)(e & 0xffu);
+#pragma unroll
+                for (int k = 0; k < kGenW; ++k)
+                    if ((e >> (8 + k)) & 1u) {
+                        const uint32_t q = (qt[(k >> 1) * 128 + gg] >> (16 * (k & 1))) & 0xffffu;
+                        atomicXor(&xb[q >> 5], 1u << (q & 31));
+                    }
             }
         }
         wave_lds_sync();
         if (lean_fin) {
             uint64_t X[XW];
 #pragma unroll
-            for (int w = 0; w < XW; ++w) X[w] = __ballot(xh[w * 64 + lane] & 1);
+            for (int w = 0; w < XW; ++w) X[w] = (uint64_t)xb[2 * w] | ((uint64_t)xb[2 * w + 1] << 32);
             int any_fail = 0;
             if (want_fail) {  // the entry carries the readout words or (q_rpar) its logical parities
                 uint64_t Rd[XW];
@@ -827,8 +862,11 @@ __global__ __launch_bounds__(64 * kLutWaves, LEAN ? kLutOcc : 4) void ssf_lut_ke
                 if (a.ssf_steps) a.ssf_steps[shot] = steps;
                 if (a.fail) a.fail[shot] = (uint8_t)any_fail;
             }
-        } else {
-            if constexpr (!LEAN) finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
+        } else if constexpr (!LEAN) {
+#pragma unroll
+            for (int w = 0; w < XW; ++w) xh[w * 64 + lane] = (uint8_t)((xb[2 * w + (lane >> 5)] >> (lane & 31)) & 1u);
+            wave_lds_sync();
+            finalize_shot(g, a, shot, xh, false, sw == 0, steps, lane);
         }
         wave_lds_sync();
         slot = slot1;
@@ -999,12 +1037,13 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             b.it1_lut = (a.ms_scaling == 0.0 && a.max_iter >= 1 && g.opt_triage_it1)
                             ? g.it1_lut[sizeof(T) == 4 ? 1 : 0]
                             : nullptr;
-            hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpSegs * 128, stream);
+            hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpLists * kCmpSegs * 128, stream);
             if (e != hipSuccess) return (int)e;
             int rc = launch_triage<RC, RV>(g, b, stream);
             if (rc != 0) return rc;
             if (b.ev) (void)hipEventRecord(b.ev[3], stream);  // end of the pre-pass
-            size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16 + 2 * 64 * 8;
+            size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16 +
+                          2 * kCmpLists * kCmpSegs * 8;
             // a capped grid (f64: 8 waves per CU) must also be placed evenly: the
             // dispatcher stacks up to the kernel's own occupancy on a CU (11 for
             // the 159-VGPR f64 kernel) while others sit idle, so the LDS request is

@@ -85,19 +85,36 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
             a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
         }
     } else if (want_fail && !walk) {
-        for (int w0 = tid; w0 < g.lz_words; w0 += kBlock) {
-            unsigned long long word = 0;
-            for (int b = 0; b < 64; ++b) {
-                const int q = w0 * 64 + b;
-                if (q >= g.n_data) break;
-                int cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
-                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
-                if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
-                if (want_fail) word |= (unsigned long long)((a.readout[shot * g.n_data + q] ^ cb) & 1) << b;
+        // dense logicals, kBlock words at a time: wave w builds words
+        // base + 64 w + i (i < 64) by ballots over coalesced byte reads and lane
+        // i keeps word i; then per logical r each lane ANDs its word with the
+        // row's (a coalesced load across the lanes), the wave folds the parities
+        // with one ballot, and one LDS XOR per wave and row accumulates them
+        const int lane = tid & 63, wv = tid >> 6;
+        for (int wbase = 0; wbase < g.lz_words; wbase += kBlock) {
+            unsigned long long mine = 0ull;
+            for (int i = 0; i < 64; ++i) {
+                const int w0 = wbase + wv * 64 + i;
+                if (w0 >= g.lz_words) break;  // uniform
+                const int q = w0 * 64 + lane;
+                int v = 0;
+                if (q < g.n_data) {
+                    int cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
+                    for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+                    if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+                    v = (a.readout[shot * g.n_data + q] ^ cb) & 1;
+                }
+                const unsigned long long word = __ballot(v);
+                mine = lane == i ? word : mine;
             }
-            if (want_fail)
-                for (int r = 0; r < g.k; ++r)
-                    if (__popcll(g.lz[(size_t)r * g.lz_words + w0] & word) & 1) atomicXor(&lpar[r], 1);
+            const int w0 = wbase + tid;
+            const bool have = w0 < g.lz_words;
+            for (int r = 0; r < g.k; ++r) {
+                const int x = have ? (__popcll(g.lz[(size_t)r * g.lz_words + w0] & mine) & 1) : 0;
+                if (__popcll(__ballot(x)) & 1) {  // uniform per wave
+                    if (lane == 0) atomicXor(&lpar[r], 1);
+                }
+            }
         }
     }
     __syncthreads();
@@ -767,10 +784,21 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
             // (per slot l a coalesced read of its shot's syndrome row)
             for (int i = tid; i < m; i += kGrpThreads) {
                 uint64_t w = sw[i] & ~need;
-                for (uint64_t rem = live; rem; rem &= rem - 1) {
-                    const int l = __builtin_ctzll(rem);
-                    const long long sl = b0 + __popcll(need & ((1ull << l) - 1ull));
-                    w |= (uint64_t)(a.syn[sl * m + i] & 1) << l;
+                // four slots per round: their loads issued before any is used
+                for (uint64_t rem = live; rem;) {
+                    int ls[4];
+                    uint8_t bv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        ls[u] = rem ? __builtin_ctzll(rem) : -1;
+                        rem &= rem - 1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        bv[u] = ls[u] >= 0 ? a.syn[(b0 + __popcll(need & ((1ull << ls[u]) - 1ull))) * m + i] : 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (ls[u] >= 0) w |= (uint64_t)(bv[u] & 1) << ls[u];
                 }
                 sw[i] = w;
             }
@@ -985,13 +1013,29 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
                     uint64_t cw = 0;
                     for (int b = 0; b < g.fold_blocks; ++b) cw ^= xw[b * nd + q];
                     uint64_t rword = 0;
-                    for (uint64_t rem = F; rem; rem &= rem - 1) {
-                        const int l = __builtin_ctzll(rem);
-                        const int64_t sl = readlane64(shot, l);
-                        int cb = (int)((cw >> l) & 1ull);
-                        if (a.base) cb ^= a.base[sl * nd + q] & 1;
-                        if (a.corr_out) a.corr_out[sl * nd + q] = (uint8_t)cb;
-                        if (want_fail) rword |= (uint64_t)((a.readout[sl * nd + q] ^ cb) & 1) << l;
+                    // four finishing slots per round, loads first
+                    for (uint64_t rem = F; rem;) {
+                        int ls[4];
+                        int64_t sls[4];
+                        uint8_t bb[4], rb[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            ls[u] = rem ? __builtin_ctzll(rem) : -1;
+                            rem &= rem - 1;
+                            sls[u] = ls[u] >= 0 ? readlane64(shot, ls[u]) : 0;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            bb[u] = (ls[u] >= 0 && a.base) ? a.base[sls[u] * nd + q] : 0;
+                            rb[u] = (ls[u] >= 0 && want_fail) ? a.readout[sls[u] * nd + q] : 0;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (ls[u] < 0) continue;
+                            const int cb = (int)((cw >> ls[u]) & 1ull) ^ (bb[u] & 1);
+                            if (a.corr_out) a.corr_out[sls[u] * nd + q] = (uint8_t)cb;
+                            if (want_fail) rword |= (uint64_t)((rb[u] ^ cb) & 1) << ls[u];
+                        }
                     }
                     if (want_fail) rw[q] = rword;
                 }
@@ -1002,7 +1046,18 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
                 uint64_t fm = 0;
                 for (int r = tid; r < g.k; r += kGrpThreads) {
                     uint64_t p = 0;
-                    for (int t = g.lz_ptr[r]; t < g.lz_ptr[r + 1]; ++t) p ^= rw[g.lz_idx[t]];
+                    const int t1 = g.lz_ptr[r + 1];
+                    int t = g.lz_ptr[r];
+                    for (; t + 4 <= t1; t += 4) {  // four supports per round, loads first
+                        int q4[4];
+                        uint64_t v4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) q4[u] = g.lz_idx[t + u];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) v4[u] = rw[q4[u]];
+                        p ^= v4[0] ^ v4[1] ^ v4[2] ^ v4[3];
+                    }
+                    for (; t < t1; ++t) p ^= rw[g.lz_idx[t]];
                     fm |= p;
                 }
                 if (fm & F) atomicOr(&s_fail, (unsigned long long)(fm & F));

@@ -784,6 +784,10 @@ struct TriageIt1 {
     static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
 };
 
+#ifndef QDEC_AB_HEAVY_W  // A/B define (round 5), removed after the measurement
+#define QDEC_AB_HEAVY_W 6
+#endif
+constexpr int kHeavyW = QDEC_AB_HEAVY_W;  // listed shots of larger syndrome weight go to the heavy list
 constexpr int kT1GateW = 12;  // iteration-1 tile gate: syndrome weight bound ...
 constexpr int kT1GateN = 8;   // ... and shots of the tile within it
 constexpr int kTriageUB = 16;  // readout-tile loads per lane per round
@@ -1006,14 +1010,25 @@ __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs
     const unsigned long long bal = __ballot(listed);
     if (bal == 0ull) return;
     // segment blockIdx % kCmpSegs: 64 counters on their own lines, so the
-    // per-tile atomics do not serialise on one address
+    // per-tile atomics do not serialise on one address.  Shots of syndrome
+    // weight > kHeavyW go to the heavy list (segments kCmpSegs..), which the BP
+    // kernel hands out first: the long decodes start at the launch's beginning
+    // instead of setting its end (longest-processing-time-first)
+    const bool heavy = listed && wt > kHeavyW;
+    const unsigned long long balh = __ballot(heavy), ball = bal & ~balh;
     const int seg = (int)(blockIdx.x % kCmpSegs);
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(a.cmp_count + 16 * seg, (unsigned long long)__popcll(bal));
-    base = __shfl(base, 0);
+    unsigned long long bh = 0, bl = 0;
+    if (lane == 0) {
+        if (balh) bh = atomicAdd(a.cmp_count + 16 * (kCmpSegs + seg), (unsigned long long)__popcll(balh));
+        if (ball) bl = atomicAdd(a.cmp_count + 16 * seg, (unsigned long long)__popcll(ball));
+    }
+    bh = __shfl(bh, 0);
+    bl = __shfl(bl, 0);
     if (listed) {
-        const uint64_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        uint64_t* e = a.cmp + ((uint64_t)seg * a.cmp_cap + base + rank) * Ent::EW;
+        const unsigned long long mb = heavy ? balh : ball;
+        const uint64_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+        const int sg = heavy ? kCmpSegs + seg : seg;
+        uint64_t* e = a.cmp + ((uint64_t)sg * a.cmp_cap + (heavy ? bh : bl) + rank) * Ent::EW;
         e[0] = (uint64_t)shot;
 #pragma unroll
         for (int rc = 0; rc < RC; ++rc) e[1 + rc] = sw[rc];
@@ -1069,32 +1084,36 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
         for (int e = lane; e < g.k * RV; e += 64) lzs[e] = g.ms_lzs[e];
     wave_lds_sync();
 
-    // chunks of KP entries inside the segments: lane s < kCmpSegs holds segment
-    // s's entry count; cend = inclusive prefix of the segments' chunk counts
+    // chunks of KP entries inside the segments, the heavy list first: virtual
+    // segment v < 64 is heavy segment v (physical kCmpSegs + v), v >= 64 light
+    // segment v - 64; lane s holds heavy and light segment s's entry counts;
+    // seg_end = inclusive prefix of the virtual segments' chunk counts
     static_assert(kCmpSegs == 64, "one lane per segment");
-    const int64_t scount = (int64_t)__builtin_nontemporal_load(a.cmp_count + 16 * lane);
+    const int64_t hcount = (int64_t)__builtin_nontemporal_load(a.cmp_count + 16 * (kCmpSegs + lane));
+    const int64_t lcount = (int64_t)__builtin_nontemporal_load(a.cmp_count + 16 * lane);
     // entries per chunk: KP, fewer when the list is short (below KP entries per
     // wave the decode is latency-bound: spread the shots over more waves)
-    int64_t tot = scount;
+    auto wave_prefix = [&](int64_t v) {
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int64_t o = (int64_t)readlane64_up((uint64_t)tot, off, lane);
-        tot += lane >= off ? o : 0;
-    }
-    tot = (int64_t)readlane64((uint64_t)tot, 63);
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t o = (int64_t)readlane64_up((uint64_t)v, off, lane);
+            v += lane >= off ? o : 0;
+        }
+        return v;
+    };
+    const int64_t tot = (int64_t)readlane64((uint64_t)wave_prefix(hcount + lcount), 63);
     const int kp = (int)min((int64_t)KP, max((int64_t)1, (tot + gridDim.x - 1) / gridDim.x));
-    int64_t cend = (scount + kp - 1) / kp;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int64_t o = (int64_t)readlane64_up((uint64_t)cend, off, lane);
-        cend += lane >= off ? o : 0;
-    }
-    const int64_t nch = (int64_t)readlane64((uint64_t)cend, 63);
+    const int64_t hend = wave_prefix((hcount + kp - 1) / kp);
+    const int64_t hch = (int64_t)readlane64((uint64_t)hend, 63);
+    const int64_t lend = hch + wave_prefix((lcount + kp - 1) / kp);
+    const int64_t nch = (int64_t)readlane64((uint64_t)lend, 63);
     // kept in LDS (read once per chunk), not in registers across the BP loop
-    int64_t* seg_end = reinterpret_cast<int64_t*>(lzs + (size_t)g.k * RV);  // [64] chunk prefix
-    int64_t* seg_cnt = seg_end + 64;                                       // [64] entries
-    seg_end[lane] = cend;
-    seg_cnt[lane] = scount;
+    int64_t* seg_end = reinterpret_cast<int64_t*>(lzs + (size_t)g.k * RV);  // [128] chunk prefix
+    int64_t* seg_cnt = seg_end + 2 * kCmpSegs;                             // [128] entries
+    seg_end[lane] = hend;
+    seg_end[kCmpSegs + lane] = lend;
+    seg_cnt[lane] = hcount;
+    seg_cnt[kCmpSegs + lane] = lcount;
     wave_lds_sync();
     // the chunk counter only pays when the tail is long (>= 16 chunks per wave)
     unsigned long long* ctr = a.wave_ctr && nch >= 16 * (int64_t)gridDim.x ? a.wave_ctr : nullptr;
@@ -1103,11 +1122,13 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
     auto load_chunk = [&](int64_t c) -> uint64_t {
         ne_n = 0;
         if (c >= nch) return 0ull;
-        const int s = __popcll(__ballot(seg_end[lane] <= c));  // the segment holding chunk c
-        const int64_t c_in = c - (s ? seg_end[s - 1] : 0);
-        const int64_t cnt = seg_cnt[s];
+        // the virtual segment holding chunk c, then its physical segment
+        const int v = __popcll(__ballot(seg_end[lane] <= c)) + __popcll(__ballot(seg_end[kCmpSegs + lane] <= c));
+        const int64_t c_in = c - (v ? seg_end[v - 1] : 0);
+        const int64_t cnt = seg_cnt[v];
         ne_n = (int)min((int64_t)kp, cnt - c_in * kp);
-        const int64_t e = ((int64_t)s * a.cmp_cap + c_in * kp) * EW + lane;
+        const int ps = v < kCmpSegs ? kCmpSegs + v : v - kCmpSegs;
+        const int64_t e = ((int64_t)ps * a.cmp_cap + c_in * kp) * EW + lane;
         return lane < ne_n * EW ? __builtin_nontemporal_load(a.cmp + e) : 0ull;
     };
     // one flat loop over this wave's entries (chunk c, entry q of it; the next

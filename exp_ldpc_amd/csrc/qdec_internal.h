@@ -19,7 +19,8 @@ constexpr int kSsfScale = 840;   // lcm(1..8): gain/|F| compared as gain*(840/|F
 constexpr int kLutLC = 16;       // table-driven SSF: max local checks per generator (16-bit local syndromes)
 constexpr int kLutLCW = kLutLC / 4;  // words of u8 local-check ids per generator
 constexpr int kEdgePad = 16;     // index / prior arrays padded past E (>= the largest row / column width)
-constexpr int kCmpSegs = 64;     // segments (and counters) of the compact shot list
+constexpr int kCmpSegs = 64;     // segments (and counters) of each compact shot list
+constexpr int kCmpLists = 2;     // the light list (segments 0..63) and the heavy list (64..127)
 // entries a compact-list segment must hold for a batch of B shots (64-shot tiles)
 inline int64_t cmp_seg_cap(int64_t B) { return ((B + 63) / 64 + kCmpSegs - 1) / kCmpSegs * 64; }
 
@@ -135,7 +136,8 @@ struct DevGraph {
     // among all positive scores (0: no positive gain).  s_lcw: the canonical local
     // checks as u8 ids, 4 per word ([kLutLCW][g_pad], pad 0xff); s_tog: per check
     // c and lane l the local-syndrome bits that toggle when c flips, generator l
-    // in the low half-word, generator 64 + l in the high one ([m_pad][64]).
+    // in the low half-word, generator 64 + l in the high one ([m_pad + 1][64],
+    // row m_pad all zero).
     const uint32_t* s_lut;
     int s_lut_n;
     const uint32_t* s_off;
@@ -221,8 +223,9 @@ struct DecodeArgs {
     // stage's pre-pass (record_ev)
     hipEvent_t* ev;    // [4] or nullptr
     // compact shot list of lean min-sum wave launches (ms_triage_kernel ->
-    // bp_ms_cmp_kernel), in kCmpSegs segments: triage tile t appends to
-    // segment t % kCmpSegs, whose entries [cmp_cap][CmpEntry::EW] u64 start at
+    // bp_ms_cmp_kernel), in kCmpLists x kCmpSegs segments: triage tile t appends
+    // to segment t % kCmpSegs (light shots) and kCmpSegs + t % kCmpSegs (heavy
+    // ones, decoded first), whose entries [cmp_cap][CmpEntry::EW] u64 start at
     // cmp + s * cmp_cap * EW, counted at cmp_count[s * 16] (one 128-B line per
     // counter; zeroed by the launcher).  nullptr -> no compact path
     uint64_t* cmp;

@@ -265,14 +265,15 @@ int qd_graph_get_option(const qd_graph* g, int32_t option, int32_t* value);
 int qd_graph_ssf_tables(const qd_graph* g, int32_t* has_lut, int64_t* lut_bytes);
 /* Copies of the table-driven SSF kernel's tables, for host-only graphs
  * (qd_graph_create_host; tests emulate the kernel's steps on them): lut
- * [lut_bytes / 4], off [g_pad], lcw [4][g_pad], tog [m_pad][64] (u32 each; the
+ * [lut_bytes / 4], off [g_pad], lcw [4][g_pad], tog [m_pad + 1][64] (u32 each; the
  * layouts of DevGraph::s_lut / s_off / s_lcw / s_tog in qdec_internal.h);
  * *g_pad and *m_pad receive the strides.  Any output may be NULL. */
 /* Host-side layout of the handle's queue scratch for a batch of B shots (the
  * workspace attach_queue allocates; tests check its alignment and capacities
  * on host-only graphs): out[8] = total bytes, offsets of the shot-index array,
  * the hard-decision / packed-entry region, the residual region, the compact
- * list's 64 segment counters and its entries, the entries per segment, the
+ * lists' 2 x 64 segment counters (light, then heavy) and their entries, the
+ * entries per segment, the
  * bytes per entry.  No reference counterpart. */
 int qd_graph_queue_layout(const qd_graph* g, int64_t B, int64_t* out);
 

@@ -392,7 +392,7 @@ def _lut_tables(lib, h):
     lut = np.zeros(nb.value // 4, np.uint32)
     off = np.zeros(gp.value, np.uint32)
     lcw = np.zeros((4, gp.value), np.uint32)
-    tog = np.zeros((mp.value, 64), np.uint32)
+    tog = np.zeros((mp.value + 1, 64), np.uint32)
     _abi.check(lib.qd_graph_ssf_tables_copy(h, _abi.ptr(lut), _abi.ptr(off), _abi.ptr(lcw), _abi.ptr(tog), None,
                                             None), "copy")
     return lut, off, lcw, tog, gp.value
@@ -415,6 +415,7 @@ def test_ssf_lut_tables_follow_the_spec(code225, oracle_lib, max_steps):
         assert tab is not None
         lut, off = tab[0], tab[1]
         assert lut.size == 4096 and not off[:hx.shape[0]].any()
+        assert not tab[3][-1].any()  # the zero toggle row the kernel reads for unflipped bits
         ranks = sorted({int(e) >> 24 for e in lut} - {0})
         assert ranks == list(range(1, len(ranks) + 1))
         rng = np.random.default_rng(11)
@@ -498,9 +499,11 @@ def test_host_only_queue_layout(code225):
             assert idx == 256 and x == idx + 8 * B and r == x + B * n
             packed = 8 * (1 + 2 * 256 // 64 + 128 // 64)
             assert cnt >= x + B * max(n + m, packed) and cnt % 256 == 0
-            assert cmp == cnt + 64 * 128 and cmp % 16 == 0 and ent % 16 == 8 and ent == 8 * (1 + 2 + 4)
+            # two lists (light, heavy) of 64 segments, every segment able to
+            # hold all of its tiles' shots
+            assert cmp == cnt + 2 * 64 * 128 and cmp % 16 == 0 and ent == 8 * (1 + 2 + 4)
             tiles = -(-B // 64)
             assert cap * 64 >= B and cap >= 64 * (-(-tiles // 64)) and cap % 64 == 0
-            assert total >= cmp + 64 * cap * ent
+            assert total >= cmp + 2 * 64 * cap * ent
     finally:
         lib.qd_graph_destroy(h)
