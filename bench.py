@@ -309,14 +309,20 @@ def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
     return res
 
 
-def c4_line(dev, shots: int = 1 << 17, ps=(0.005, 0.01, 0.03), precisions=("f64", "f32")):
+def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64", "f32")):
     """BASELINE config 4's code on one GPU (the driver's record of it; the
     config itself shards 1e7 shots over 8 GPUs exactly as the headline does):
     biregular_hgp(80, 3, 4, seed=2025), n = 10^4 (reference-generated checks,
     tests/golden/hgp_80_3_4_s2025_checks.npz; logicals fixture from
     tools/fixtures/make_c4_logicals.py), R = 0, BP min-sum max_iter 50 + SSF +
     logical check.  Per (precision, p): one warmup launch and one timed launch
-    of `shots` device-sampled shots, HIP events around the BP and SSF kernels.
+    of `shots` device-sampled shots (2^19 at p <= 0.01, 2^18 at higher p),
+    HIP events around the BP and SSF kernels.  The batch is large because the
+    slot-group kernel's launch ends with each group's last shots: a group keeps
+    streaming all 64 slots' lines while its slowest shot (up to 50 iterations)
+    finishes, and at low p (2-6 iterations per shot) that tail weighs against
+    2^17 / 256 groups = 512 shots per group; the config itself decodes 1e7
+    shots.
     f64 runs the slot-group kernel (messages stream through HBM: HBM roofline,
     32 B per edge per shot-iteration + I/O); f32 runs the LDS-resident kernel
     (every message on chip: LDS roofline, per shot-iteration 20 B per edge --
@@ -335,7 +341,9 @@ def c4_line(dev, shots: int = 1 << 17, ps=(0.005, 0.01, 0.03), precisions=("f64"
     m, n = hz.shape
     E = int(hz.nnz)
     lines = []
+    full = shots
     for p in ps:
+        shots = full if p <= 0.01 else full // 2
         sampler = Decoder(hz, 2 * p / 3, method="ms", precision="f32", max_iter=50, device=dev.index)
         syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
         rd = torch.empty((2, shots, n), dtype=torch.uint8, device=dev)
@@ -384,7 +392,8 @@ def c4_line(dev, shots: int = 1 << 17, ps=(0.005, 0.01, 0.03), precisions=("f64"
         torch.cuda.empty_cache()
     return {"config": "C4: biregular_hgp(80,3,4,seed=2025), n=10000 (BASELINE configs[3]'s code; 1 GPU, the "
                       "headline's shot sharding carries it to 8), R=0, BP min-sum max_iter 50 + SSF + logical check, "
-                      f"{shots} device-sampled shots per timed launch", "m": m, "n": n, "E": E, "lines": lines}
+                      f"{full} device-sampled shots per timed launch at p <= 0.01, {full // 2} above",
+            "m": m, "n": n, "E": E, "lines": lines}
 
 
 def reference_default_line(dev, code, shots: int = 1 << 18, batch: int = 1 << 16, p: float = 0.01,
