@@ -507,3 +507,43 @@ def test_host_only_queue_layout(code225):
             assert total >= cmp + 2 * 64 * cap * ent
     finally:
         lib.qd_graph_destroy(h)
+
+
+def test_kernel_options_are_handle_state_not_environment(code225):
+    """Kernel choices are per-handle options (qd_graph_set_option): defaults,
+    round trip, range checks, unknown options refused; and no source file of
+    the library reads the environment (every knob of earlier rounds that
+    switched a kernel per launch by getenv is gone or an option)."""
+    import ctypes as C
+    import glob
+    import os
+    import re
+
+    from exp_ldpc_amd import _abi
+    from exp_ldpc_amd.decoder import OPTIONS
+    from conftest import REPO
+    lib = _abi.load()
+    h, _, _ = _host_graph(lib, code225.checks.z, gens=code225.checks.x, probs=0.01)
+    try:
+        v = C.c_int32(0)
+        defaults = {"compact": 1, "triage_it1": 1, "ssf": 0, "lds_kernel": -1, "group_kernel": -1, "ssf_inc": 1,
+                    "block_wg": 0, "group_mb": 0}
+        for name, d in defaults.items():
+            _abi.check(lib.qd_graph_get_option(h, OPTIONS[name], C.byref(v)), name)
+            assert v.value == d, name
+        for name, val in (("compact", 0), ("ssf", 3), ("lds_kernel", 1), ("group_mb", 512)):
+            _abi.check(lib.qd_graph_set_option(h, OPTIONS[name], val), name)
+            _abi.check(lib.qd_graph_get_option(h, OPTIONS[name], C.byref(v)), name)
+            assert v.value == val
+        assert lib.qd_graph_set_option(h, OPTIONS["ssf"], 4) == -2
+        assert lib.qd_graph_set_option(h, OPTIONS["compact"], 2) == -2
+        assert lib.qd_graph_set_option(h, 99, 0) == -2
+        has, nb = C.c_int32(0), C.c_int64(0)
+        _abi.check(lib.qd_graph_ssf_tables(h, C.byref(has), C.byref(nb)), "tables")
+        assert has.value == 1 and nb.value == 4096 * 4
+    finally:
+        lib.qd_graph_destroy(h)
+    srcs = glob.glob(os.path.join(REPO, "exp_ldpc_amd", "csrc", "*"))
+    assert srcs
+    for f in srcs:
+        assert not re.search(r"\bgetenv\s*\(", open(f).read()), f
