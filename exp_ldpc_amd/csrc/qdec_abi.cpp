@@ -1081,12 +1081,15 @@ static void ssf_lut_tables(qd_graph* G, int n_gen, const int32_t* gen_ptr, const
     DevGraph& g = G->dg;
     g.s_lut = g.s_off = g.s_lcw = g.s_tog = nullptr;
     g.s_lut_n = 0;
-    if (n_gen > 128 || g.m_pad > 255) return;
+    // the wave kernel's per-lane tables (u8 check ids, toggle rows by lane);
+    // the workgroup SSF kernel reads only the score tables and offsets
+    const bool lanes = n_gen <= 128 && g.m_pad <= 255;
+    if (n_gen >= 8192) return;
     std::vector<std::vector<uint32_t>> shapes;  // (w, nlc, M_0 .. M_{w-1}) in first-seen order
     std::vector<int> shape_off;
     std::vector<uint32_t> off(gp, 0);
     std::vector<uint32_t> lcw((size_t)kLutLCW * gp, 0xffffffffu);
-    std::vector<uint32_t> tog(((size_t)g.m_pad + 1) * 64, 0);  // row m_pad: zero (the kernel's unflipped bits)
+    std::vector<uint32_t> tog(lanes ? ((size_t)g.m_pad + 1) * 64 : 0, 0);  // row m_pad: zero (unflipped bits)
     int total = 0;
     for (int gi = 0; gi < n_gen; ++gi) {
         const int a = gen_ptr[gi], w = gen_ptr[gi + 1] - a;
@@ -1123,14 +1126,16 @@ static void ssf_lut_tables(qd_graph* G, int n_gen, const int32_t* gen_ptr, const
             o = shape_off[it - shapes.begin()];
         }
         off[gi] = (uint32_t)o;
-        for (int b = 0; b < nlc; ++b) {
-            const int c = sig[b].first;
-            uint32_t& word = lcw[(size_t)(b / 4) * gp + gi];
-            word = (word & ~(0xffu << (8 * (b % 4)))) | ((uint32_t)c << (8 * (b % 4)));
-            tog[(size_t)c * 64 + (gi & 63)] |= (1u << b) << (16 * (gi >> 6));
-        }
+        if (lanes)
+            for (int b = 0; b < nlc; ++b) {
+                const int c = sig[b].first;
+                uint32_t& word = lcw[(size_t)(b / 4) * gp + gi];
+                word = (word & ~(0xffu << (8 * (b % 4)))) | ((uint32_t)c << (8 * (b % 4)));
+                tog[(size_t)c * 64 + (gi & 63)] |= (1u << b) << (16 * (gi >> 6));
+            }
     }
-    if ((size_t)total * 4 + ((size_t)g.m_pad + 1) * 256 > kLutBudget) return;
+    if ((size_t)total * 4 > kLutBudget) return;
+    const bool lane_tabs = lanes && (size_t)total * 4 + ((size_t)g.m_pad + 1) * 256 <= kLutBudget;
     // best (score, t) of every local syndrome of every shape; scores -> ranks
     std::vector<int> score(total, 0);
     std::vector<uint32_t> lut(total, 0);
@@ -1165,8 +1170,10 @@ static void ssf_lut_tables(qd_graph* G, int n_gen, const int32_t* gen_ptr, const
     g.s_lut = G->flip_arena.upload(lut);
     g.s_lut_n = total;
     g.s_off = G->flip_arena.upload(off);
-    g.s_lcw = G->flip_arena.upload(lcw);
-    g.s_tog = G->flip_arena.upload(tog);
+    if (lane_tabs) {
+        g.s_lcw = G->flip_arena.upload(lcw);
+        g.s_tog = G->flip_arena.upload(tog);
+    }
 }
 
 int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, const int32_t* gen_idx) {
@@ -1191,15 +1198,26 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
             if (b < a) throw Fail(-31, "gen_ptr not monotone");
             const int wg = b - a;
             if (wg > kGenW) throw Fail(-32, "flip-set generator weight exceeds 8");
-            std::vector<int> checks;
+            // local checks in the canonical order of ssf_lut_tables: by signature
+            // (the bitmask of this generator's qubit positions touching the
+            // check), ties by check id.  The spec does not depend on the order
+            // (it is internal to the local-syndrome words), and with it every
+            // kernel's local syndrome indexes the shared score tables directly.
+            std::vector<std::pair<uint32_t, int>> sig;  // (signature, check)
             for (int k = 0; k < wg; ++k) {
                 const int qq = gen_idx[a + k];
                 if (qq < 0 || qq >= g.n) throw Fail(-33, "flip-set qubit out of range");
                 if (k > 0 && qq <= gen_idx[a + k - 1]) throw Fail(-34, "flip-set qubits must be strictly ascending");
-                for (int t = G->col_ptr[qq]; t < G->col_ptr[qq + 1]; ++t) checks.push_back(G->col_rows[t]);
+                for (int t = G->col_ptr[qq]; t < G->col_ptr[qq + 1]; ++t) {
+                    const int c = G->col_rows[t];
+                    auto it = std::find_if(sig.begin(), sig.end(), [c](const auto& e) { return e.second == c; });
+                    if (it == sig.end()) sig.push_back({1u << k, c});
+                    else it->first ^= 1u << k;
+                }
             }
-            std::sort(checks.begin(), checks.end());
-            checks.erase(std::unique(checks.begin(), checks.end()), checks.end());
+            std::sort(sig.begin(), sig.end());
+            std::vector<int> checks;
+            for (const auto& e : sig) checks.push_back(e.second);
             if ((int)checks.size() > kGenLC) throw Fail(-35, "flip-set generator touches more than 32 checks");
             w[gi] = (uint8_t)wg;
             nlc[gi] = (uint8_t)checks.size();
@@ -1213,13 +1231,10 @@ int qd_graph_set_flipsets(qd_graph* G, int32_t n_gen, const int32_t* gen_ptr, co
                 word = (word & ~(0xffu << (8 * (c % 4)))) | ((uint32_t)checks[c] << (8 * (c % 4)));
             }
             for (int k = 0; k < wg; ++k) {
-                const int qq = gen_idx[a + k];
-                q[(size_t)k * gp + gi] = (uint16_t)qq;
+                q[(size_t)k * gp + gi] = (uint16_t)gen_idx[a + k];
                 uint32_t mask = 0;
-                for (int t = G->col_ptr[qq]; t < G->col_ptr[qq + 1]; ++t) {
-                    const int c = (int)(std::lower_bound(checks.begin(), checks.end(), G->col_rows[t]) - checks.begin());
-                    mask ^= 1u << c;
-                }
+                for (size_t c = 0; c < sig.size(); ++c)
+                    if ((sig[c].first >> k) & 1u) mask |= 1u << c;
                 qm[(size_t)k * gp + gi] = mask;
             }
         }
@@ -1740,7 +1755,7 @@ int qd_graph_get_option(const qd_graph* G, int32_t option, int32_t* value) {
 int qd_graph_ssf_tables(const qd_graph* G, int32_t* has_lut, int64_t* lut_bytes) {
     return guarded([&] {
         check_graph(G);
-        if (has_lut) *has_lut = G->dg.s_lut ? 1 : 0;
+        if (has_lut) *has_lut = G->dg.s_lut ? (G->dg.s_tog ? 1 : 2) : 0;
         if (lut_bytes) *lut_bytes = G->dg.s_lut ? (int64_t)G->dg.s_lut_n * 4 : 0;
     });
 }
@@ -1751,7 +1766,7 @@ int qd_graph_ssf_tables_copy(const qd_graph* G, uint32_t* lut, uint32_t* off, ui
         check_graph(G);
         if (!G->host_only) throw Fail(-16, "table copies are kept for host-only graphs (qd_graph_create_host)");
         const DevGraph& g = G->dg;
-        if (!g.s_lut) throw Fail(-36, "the graph has no table-driven SSF tables");
+        if (!g.s_lut || !g.s_tog) throw Fail(-36, "the graph has no table-driven wave SSF tables");
         if (g_pad) *g_pad = g.g_pad;
         if (m_pad) *m_pad = g.m_pad;
         auto put = [](uint32_t* dst, const uint32_t* src, size_t n) {

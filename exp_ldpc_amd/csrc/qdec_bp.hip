@@ -1139,7 +1139,7 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hip
             if (e2 != hipSuccess) return (int)e2;
             ss = a.ssf_stream;
         }
-        if (g.s_lut && g.opt_ssf == kSsfAuto) {
+        if (g.s_lut && g.s_tog && g.opt_ssf == kSsfAuto) {
             rc = g.n_gen <= 64 ? launch_ssf_lut<1, RV, RC>(g, a, num_cus, ss)
                                : launch_ssf_lut<2, RV, RC>(g, a, num_cus, ss);
         } else {

@@ -556,10 +556,19 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
     for (int w = tid; w < (int)((gp + 31) / 32); w += kBlock) dbits[w] = 0u;
     if (tid == 0) ctl[0] = 0;
+    // table scoring (DevGraph::s_lut, ssf_lut_tables): a generator's best
+    // (score, subset) is one lookup on its local syndrome; the key then carries
+    // the score's rank, which orders like the score
+    const bool lut = g.s_lut && g.opt_ssf == kSsfAuto;
     auto rescore = [&](int gi) {
         const uint32_t sl = slg[gi];
         if (sl == 0u) {
             key[gi] = INT_MIN;
+            return;
+        }
+        if (lut) {
+            const uint32_t r = g.s_lut[g.s_off[gi] + sl] >> 24;
+            key[gi] = r ? (int)((r << 13) | (uint32_t)(8191 - gi)) : INT_MIN;
             return;
         }
         uint32_t qm[kGenW];
@@ -598,7 +607,14 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
                 if (best == LLONG_MIN || kv == INT_MIN || score <= 0) break;
                 const int gsel = 8191 - (kv & 8191);
                 const int w = g.g_w[gsel];
-                if (tid < 64) {  // wave 0: the lowest subset reaching the score
+                if (lut) {  // the table entry names the subset and the local checks it toggles
+                    if (tid == 0) {
+                        const uint32_t sl = slg[gsel];
+                        const uint32_t e = g.s_lut[g.s_off[gsel] + sl];
+                        ctl[1] = (int)(e & 0xffu);
+                        ctl[2] = __builtin_popcount(sl) - __builtin_popcount(sl ^ ((e >> 8) & 0xffffu));  // gain
+                    }
+                } else if (tid < 64) {  // wave 0: the lowest subset reaching the score
                     const uint32_t sl = slg[gsel];
                     const int base = __builtin_popcount(sl);
                     uint32_t qs[kGenW];
@@ -623,10 +639,12 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
                 __syncthreads();
                 const int tsel = ctl[1];
                 if (tsel <= 0) break;  // unreachable: the best score is some subset's score
-                const int gain = score * __builtin_popcount(tsel) / kSsfScale;
                 uint32_t mask = 0;
                 for (int k = 0; k < w; ++k)
                     if ((tsel >> k) & 1) mask ^= g.g_qmask[k * gp + gsel];
+                // (read before any thread's flip below changes slg: set by tid 0
+                // before the barrier)
+                const int gain = lut ? ctl[2] : score * __builtin_popcount(tsel) / kSsfScale;
                 // flip: residual, hard decision, and every generator's local syndrome
                 // bit of each flipped check (those generators are queued for re-scoring)
                 if (tid < g.g_nlc[gsel] && ((mask >> tid) & 1)) {

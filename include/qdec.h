@@ -228,9 +228,10 @@ int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int3
  *                        shot triage + compact-list kernel; 0: the one-pass kernel.
  *   QD_OPT_TRIAGE_IT1    1 (default): the triage runs min-sum iteration 1
  *                        bit-sliced (default alpha schedule, positive priors); 0: off.
- *   QD_OPT_SSF           SSF kernel of wave graphs: QD_SSF_AUTO (default: the
- *                        table-driven kernel when the graph's tables qualify, else
- *                        the scanning kernel), QD_SSF_SCAN (scanning kernel,
+ *   QD_OPT_SSF           SSF kernels: QD_SSF_AUTO (default: the table-driven
+ *                        wave kernel, or table scoring in the workgroup kernel,
+ *                        when the graph's tables qualify, else the scanning
+ *                        kernels), QD_SSF_SCAN (scanning kernel / subset search,
  *                        incremental local syndromes), QD_SSF_SCAN_GATHER (scanning
  *                        kernel, local syndromes re-gathered every step),
  *                        QD_SSF_SCAN_NOSPLIT (scanning, one lane per generator).
@@ -258,10 +259,11 @@ int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int3
 int qd_graph_set_option(qd_graph* g, int32_t option, int32_t value);
 int qd_graph_get_option(const qd_graph* g, int32_t option, int32_t* value);
 
-/* Which SSF kernel the handle's graph qualifies for on its own: 1 when the
- * table-driven kernel's tables were built (QD_SSF_AUTO then runs it), 0
- * otherwise.  *lut_bytes (nullable) = bytes of its score tables.  No reference
- * counterpart. */
+/* Which table-driven SSF the handle's graph qualifies for: 1 when the wave
+ * kernel's tables were built (ssf_lut_kernel: QD_SSF_AUTO then runs it), 2 when
+ * only the score tables were (graphs beyond the wave shapes: the workgroup SSF
+ * kernel scores generators by table lookup), 0 otherwise.  *lut_bytes
+ * (nullable) = bytes of the score tables.  No reference counterpart. */
 int qd_graph_ssf_tables(const qd_graph* g, int32_t* has_lut, int64_t* lut_bytes);
 /* Copies of the table-driven SSF kernel's tables, for host-only graphs
  * (qd_graph_create_host; tests emulate the kernel's steps on them): lut

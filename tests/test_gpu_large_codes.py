@@ -229,6 +229,26 @@ def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatc
         _decode_both(oracle_lib, H, probs, syn, max_iter=30, ms_scaling=scaling)
 
 
+@pytest.mark.parametrize("scoring", ["auto", "scan"])
+def test_hgp10k_ssf_table_scoring_parity(gpu_available, oracle_lib, hgp10k, scoring, monkeypatch):
+    """The incremental workgroup SSF kernel scores generators by table lookup
+    when the graph's score tables qualify (every generator of this HGP code
+    shares one 4096-entry table; QD_SSF_AUTO) or by the subset search
+    (QD_SSF_SCAN): both equal the oracle, f32 and f64."""
+    from exp_ldpc_amd.decoder import Decoder
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "ssf", scoring)
+    hx, hz, lz = hgp10k
+    d = Decoder(hz, 0.02, method="ms", precision="f32", max_iter=5, flip_sets=hx)
+    assert d.ssf_tables() == (True, 4096 * 4)  # score tables only (beyond the wave shapes)
+    assert d.get_option("ssf") == (0 if scoring == "auto" else 1)
+    p = 0.03
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=17, shot0=0, B=128)
+    for precision in ("f32", "f64"):
+        got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=30, keys=KEYS_SSF,
+                           precision=precision)
+        assert got["ssf_steps"].sum() > 0
+
+
 def test_hgp10k_ssf_rescan_kernel_parity(gpu_available, oracle_lib, hgp10k, monkeypatch):
     """The re-scanning SSF block kernel (QD_OPT_SSF_INC = 0) stays covered; the
     default incremental one is covered by every other C4 test."""
