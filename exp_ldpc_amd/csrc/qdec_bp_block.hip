@@ -53,6 +53,24 @@ __device__ int block_sum_i32(int v, int* red) {
     return r;
 }
 
+// dst[0..len) = src[0..len) (byte arrays, thread-strided), eight loads per
+// thread issued before the stores; returns this thread's sum of the bytes
+__device__ __forceinline__ int copy_bytes8(const uint8_t* src, uint8_t* dst, int len, int tid) {
+    int sum = 0;
+    for (int j0 = tid; j0 < len; j0 += 8 * kBlock) {
+        uint8_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = j0 + u * kBlock < len ? src[j0 + u * kBlock] : (uint8_t)0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (j0 + u * kBlock < len) {
+                dst[j0 + u * kBlock] = v[u];
+                sum += v[u];
+            }
+    }
+    return sum;
+}
+
 // Outputs of one shot from its hard decision xh (LDS): x_out, corr = base ^
 // fold(xh), fail = any_r parity(lz[r] & (readout ^ corr)) (per-thread word parities
 // xor-reduced into LDS), status, ssf_steps.
@@ -93,19 +111,32 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
         const int lane = tid & 63, wv = tid >> 6;
         for (int wbase = 0; wbase < g.lz_words; wbase += kBlock) {
             unsigned long long mine = 0ull;
-            for (int i = 0; i < 64; ++i) {
-                const int w0 = wbase + wv * 64 + i;
-                if (w0 >= g.lz_words) break;  // uniform
-                const int q = w0 * 64 + lane;
-                int v = 0;
-                if (q < g.n_data) {
-                    int cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
-                    for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
-                    if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
-                    v = (a.readout[shot * g.n_data + q] ^ cb) & 1;
+            for (int i0 = 0; i0 < 64; i0 += 8) {
+                if (wbase + wv * 64 + i0 >= g.lz_words) break;  // uniform
+                // eight words per round: their readout / base bytes loaded first
+                uint8_t rv[8], bv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int q = (wbase + wv * 64 + i0 + u) * 64 + lane;
+                    const bool in = q < g.n_data && wbase + wv * 64 + i0 + u < g.lz_words;
+                    rv[u] = in ? a.readout[shot * g.n_data + q] : (uint8_t)0;
+                    bv[u] = (in && a.base) ? a.base[shot * g.n_data + q] : (uint8_t)0;
                 }
-                const unsigned long long word = __ballot(v);
-                mine = lane == i ? word : mine;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int w0 = wbase + wv * 64 + i0 + u;
+                    if (w0 >= g.lz_words) break;  // uniform
+                    const int q = w0 * 64 + lane;
+                    int v = 0;
+                    if (q < g.n_data) {
+                        int cb = bv[u] & 1;
+                        for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
+                        if (a.corr_out) a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
+                        v = (rv[u] ^ cb) & 1;
+                    }
+                    const unsigned long long word = __ballot(v);
+                    mine = lane == i0 + u ? word : mine;
+                }
             }
             const int w0 = wbase + tid;
             const bool have = w0 < g.lz_words;
@@ -481,13 +512,11 @@ __global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArg
         const int64_t qv = a.q_idx[slot];
         const int64_t shot = qv & ((1ll << 62) - 1);
         const bool bp_conv = (qv >> 62) & 1;
-        for (int j = tid; j < n; j += kBlock) xh[j] = a.q_x[(int64_t)slot * n + j];
-        int wl = 0;
-        for (int i = tid; i < m; i += kBlock) {
-            const uint8_t r = a.q_r[(int64_t)slot * m + i];
-            sres[i] = r;
-            wl += r;
-        }
+        // the queued hard decision and residual, eight loads in flight per
+        // thread before any LDS store (a loop of single byte loads waited for
+        // each one: ~40 HBM round trips per shot at n = 10^4)
+        copy_bytes8(a.q_x + (int64_t)slot * n, xh, n, tid);
+        int wl = copy_bytes8(a.q_r + (int64_t)slot * m, sres, m, tid);
         int sw = block_sum_i32(wl, redi);  // includes a barrier: LDS fills visible
         int steps = 0;
         while (a.ssf && sw > 0 && (a.ssf_max_steps <= 0 || steps < a.ssf_max_steps)) {
@@ -580,13 +609,11 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
         const int64_t qv = a.q_idx[slot];
         const int64_t shot = qv & ((1ll << 62) - 1);
         const bool bp_conv = (qv >> 62) & 1;
-        for (int j = tid; j < n; j += kBlock) xh[j] = a.q_x[(int64_t)slot * n + j];
-        int wl = 0;
-        for (int i = tid; i < m; i += kBlock) {
-            const uint8_t r = a.q_r[(int64_t)slot * m + i];
-            sres[i] = r;
-            wl += r;
-        }
+        // the queued hard decision and residual, eight loads in flight per
+        // thread before any LDS store (a loop of single byte loads waited for
+        // each one: ~40 HBM round trips per shot at n = 10^4)
+        copy_bytes8(a.q_x + (int64_t)slot * n, xh, n, tid);
+        int wl = copy_bytes8(a.q_r + (int64_t)slot * m, sres, m, tid);
         int sw = block_sum_i32(wl, redi);  // includes a barrier: LDS fills visible
         int steps = 0;
         if (a.ssf && sw > 0) {

@@ -784,10 +784,7 @@ struct TriageIt1 {
     static constexpr size_t bytes = 8 * (size_t)(RC * 64 + 1 + RV * 64 + 1 + 64 * kMaxLogicalRounds) + 16;
 };
 
-#ifndef QDEC_AB_HEAVY_W  // A/B define (round 5), removed after the measurement
-#define QDEC_AB_HEAVY_W 6
-#endif
-constexpr int kHeavyW = QDEC_AB_HEAVY_W;  // listed shots of larger syndrome weight go to the heavy list
+constexpr int kHeavyW = 6;  // listed shots of larger syndrome weight go to the heavy list
 constexpr int kT1GateW = 12;  // iteration-1 tile gate: syndrome weight bound ...
 constexpr int kT1GateN = 8;   // ... and shots of the tile within it
 constexpr int kTriageUB = 16;  // readout-tile loads per lane per round

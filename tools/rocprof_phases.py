@@ -36,7 +36,9 @@ def main():
     by = defaultdict(list)
     with open(trace) as fh:
         for r in csv.DictReader(fh):
-            by[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            k = r["Kernel_Name"].strip()
+            k = k[5:] if k.startswith("void ") else k  # rocprof prefixes templated kernels with their return type
+            by[k].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     res = {"trace": trace, "bench": bench, "points": P, "warmup": W, "steps": K, "iso_steps": iso, "kernels": {}}
 
     def summ(v):
