@@ -325,9 +325,10 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
     shots.
     f64 runs the slot-group kernel (messages stream through HBM: HBM roofline,
     32 B per edge per shot-iteration + I/O); f32 runs the LDS-resident kernel
-    (every message on chip: LDS roofline, per shot-iteration 20 B per edge --
-    16 B state gather + 4 B v2c scatter -- and 48 B per check -- 32 B row read +
-    16 B state write)."""
+    (every message on chip: LDS roofline, per shot-iteration 8 B per edge -- the
+    variable pass reads the edge's c2v slot and writes its v2c back -- and 64 B
+    per check -- the check pass reads its 32-B row of v2c and writes it back as
+    c2v)."""
     import scipy.sparse as sp
     import torch
     from exp_ldpc_amd.decoder import Decoder
@@ -375,10 +376,10 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
                         "bytes_model": "32 B per edge per shot-iteration (f64 messages through HBM: v2c read + c2v "
                                        "write, c2v read + v2c write) + per-shot I/O"}
             else:
-                algo = (20 * E + 48 * m) * it_sum
+                algo = (8 * E + 64 * m) * it_sum
                 roof = {"bound": "lds", "peak": LDS_PEAK_GBS,
-                        "bytes_model": "LDS: 20 B per edge + 48 B per check per shot-iteration (state gather + v2c "
-                                       "scatter; row read + state write)"}
+                        "bytes_model": "LDS: 8 B per edge + 64 B per check per shot-iteration (variable pass: c2v "
+                                       "slot read + v2c write; check pass: 32-B row read + c2v row write)"}
             ach = algo / (float(bp_ms[0]) * 1e-3) / 1e9
             roof.update({"achieved": ach, "unit": "GB/s", "frac": ach / roof["peak"], "algorithmic_bytes_per_launch": algo,
                          "traffic": None})

@@ -960,6 +960,8 @@ int qd_graph_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t*
             G->dg.lz = nullptr;
             G->dg.lz_ptr = G->dg.lz_idx = nullptr;
             G->dg.lz_sparse = 0;
+            G->dg.lz_t = nullptr;
+            G->dg.lz_tw = 0;
             G->dg.n_gen = 0;
             G->dg.g_inv = nullptr;
             G->dg.g_invd = G->dg.g_invl = 0;
@@ -1006,6 +1008,8 @@ int qd_graph_create_host(int32_t m, int32_t n, const int32_t* row_ptr, const int
             G->dg.lz = nullptr;
             G->dg.lz_ptr = G->dg.lz_idx = nullptr;
             G->dg.lz_sparse = 0;
+            G->dg.lz_t = nullptr;
+            G->dg.lz_tw = 0;
             G->dg.n_gen = 0;
             G->dg.g_inv = nullptr;
             G->dg.g_invd = G->dg.g_invl = 0;
@@ -1294,6 +1298,8 @@ static void upload_logicals(qd_graph* G, int32_t k, std::vector<int32_t> ptr, st
     g.lz = nullptr;
     g.lz_ptr = g.lz_idx = nullptr;
     g.ms_lzs = nullptr;
+    g.lz_t = nullptr;
+    g.lz_tw = 0;
     g.k = 0;
     g.lz_sparse = 0;
     if (k == 0) return;
@@ -1319,6 +1325,14 @@ static void upload_logicals(qd_graph* G, int32_t k, std::vector<int32_t> ptr, st
     }
     g.lz_ptr = G->lz_arena.upload(cptr);
     g.lz_idx = G->lz_arena.upload(cidx);
+    const int tw = (k + 31) / 32;
+    if ((size_t)g.n_data * tw * 4 <= ((size_t)64 << 20)) {
+        std::vector<uint32_t> tr((size_t)g.n_data * tw, 0u);
+        for (int r = 0; r < k; ++r)
+            for (int t = cptr[r]; t < cptr[r + 1]; ++t) tr[(size_t)cidx[t] * tw + r / 32] |= 1u << (r % 32);
+        g.lz_t = G->lz_arena.upload(tr);
+        g.lz_tw = tw;
+    }
     // wave graphs: the same logicals in the min-sum kernel's lane-slot order
     // ([k][n_pad/64] words, bit s%64 of word s/64 = the column of slot s), so the
     // compact-list kernel tests its ballot words without a column permutation

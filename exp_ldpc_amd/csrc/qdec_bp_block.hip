@@ -83,7 +83,36 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
     if (want_fail)
         for (int r = tid; r < g.k; r += kBlock) lpar[r] = 0;
     __syncthreads();
-    const bool walk = want_fail && g.lz_sparse;
+    // by qubit (DevGraph::lz_t): lpar holds lz_tw parity words; each residual one
+    // XORs its qubit's words in
+    const bool cols = want_fail && g.lz_t;
+    const bool walk = want_fail && !cols && g.lz_sparse;
+    if (cols) {
+        uint32_t* lw = reinterpret_cast<uint32_t*>(lpar);  // lz_tw <= k words, zeroed above
+        const int nd = g.n_data, tw = g.lz_tw;
+        for (int q0 = tid; q0 < nd; q0 += 8 * kBlock) {
+            uint8_t rv[8], bv[8];  // eight qubits per round, their loads first
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u * kBlock;
+                rv[u] = q < nd ? a.readout[shot * nd + q] : (uint8_t)0;
+                bv[u] = (q < nd && a.base) ? a.base[shot * nd + q] : (uint8_t)0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u * kBlock;
+                if (q >= nd) break;
+                int cb = bv[u] & 1;
+                for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * nd + q];
+                if (a.corr_out) a.corr_out[shot * nd + q] = (uint8_t)cb;
+                if ((rv[u] ^ cb) & 1)
+                    for (int t = 0; t < tw; ++t) {
+                        const uint32_t v = g.lz_t[(size_t)q * tw + t];
+                        if (v) atomicXor(&lw[t], v);
+                    }
+            }
+        }
+    }
     if (walk) {  // sparse logicals: each thread tests whole logicals on their supports
         for (int r = tid; r < g.k; r += kBlock) {
             int par = 0;
@@ -96,13 +125,13 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
             lpar[r] = par;
         }
     }
-    if (a.corr_out && (!want_fail || walk)) {
+    if (a.corr_out && !cols && (!want_fail || walk)) {
         for (int q = tid; q < g.n_data; q += kBlock) {
             int cb = a.base ? (a.base[shot * g.n_data + q] & 1) : 0;
             for (int t = 0; t < g.fold_blocks; ++t) cb ^= xh[t * g.n_data + q];
             a.corr_out[shot * g.n_data + q] = (uint8_t)cb;
         }
-    } else if (want_fail && !walk) {
+    } else if (want_fail && !cols && !walk) {
         // dense logicals, kBlock words at a time: wave w builds words
         // base + 64 w + i (i < 64) by ballots over coalesced byte reads and lane
         // i keeps word i; then per logical r each lane ANDs its word with the
@@ -151,8 +180,8 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
     __syncthreads();
     int f = 0;
     if (want_fail)
-        for (int r = tid; r < g.k; r += kBlock) f |= lpar[r];
-    f = __syncthreads_or(f);
+        for (int r = tid; r < g.k; r += kBlock) f |= lpar[r] != 0;
+    f = __syncthreads_or(f) ? 1 : 0;
     if (tid == 0) {
         if (a.status) a.status[shot] = (uint8_t)((conv ? 1 : 0) | (satisfied ? 2 : 0));
         if (a.ssf_steps) a.ssf_steps[shot] = steps;
@@ -756,6 +785,7 @@ template <typename T, int DC>
 constexpr int grp_uv() {
     return sizeof(T) == 4 ? (DC <= 4 ? 16 : 8) : (DC <= 4 ? 8 : 4);
 }
+constexpr int kLzTGrp = 16;           // logical-parity words per slot in the group kernel (k <= 512)
 constexpr int kFinPerCu = 8;          // SSF/finalize workgroups per CU when their state is in HBM
 constexpr size_t kGrpHeader = 256;    // scratch header: the shot counter
 
@@ -797,6 +827,8 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
     __shared__ unsigned long long s_bad, s_fail;
     __shared__ long long s_base;
     __shared__ int s_qbase;
+    // per slot the logical-parity words of its residual (DevGraph::lz_t)
+    __shared__ uint32_t s_lp[64 * kLzTGrp];
     // wave index as a scalar: the graph index loads of the passes are scalar loads
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), tid = threadIdx.x;
     const int m = g.m, n = g.n, nd = g.n_data;
@@ -811,6 +843,8 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
     uint64_t* rw = reinterpret_cast<uint64_t*>(blk + L.rw);
     const uint64_t below = (1ull << lane) - 1ull;
     const bool want_fail = a.fail && a.readout && g.k > 0;
+    const bool lzcols = want_fail && g.lz_t && g.lz_tw <= kLzTGrp;
+    for (int i = tid; i < 64 * kLzTGrp; i += kGrpThreads) s_lp[i] = 0u;  // (the refill's barrier orders it)
     int64_t shot = -1;  // slot `lane`'s shot: identical in every wave (all decisions are group-uniform)
     int it = 0;
     uint64_t need = ~0ull;  // slots to refill (uniform)
@@ -1082,10 +1116,32 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
                             if (want_fail) rword |= (uint64_t)((rb[u] ^ cb) & 1) << ls[u];
                         }
                     }
-                    if (want_fail) rw[q] = rword;
+                    if (lzcols) {  // the residual's ones XOR their qubit's parity words into their slots'
+                        if (rword)
+                            for (int t = 0; t < g.lz_tw; ++t) {
+                                const uint32_t v = g.lz_t[(size_t)q * g.lz_tw + t];
+                                if (v)
+                                    for (uint64_t rem = rword; rem; rem &= rem - 1)
+                                        atomicXor(&s_lp[__builtin_ctzll(rem) * kLzTGrp + t], v);
+                            }
+                    } else if (want_fail) {
+                        rw[q] = rword;
+                    }
                 }
             }
-            if (want_fail) {
+            if (lzcols) {
+                __syncthreads();  // parity words complete
+                if (wv == 0) {
+                    uint32_t o = 0;
+                    for (int t = 0; t < g.lz_tw; ++t) {
+                        o |= s_lp[lane * kLzTGrp + t];
+                        s_lp[lane * kLzTGrp + t] = 0u;
+                    }
+                    const uint64_t fb = __ballot(o != 0u);
+                    if (lane == 0) s_fail = fb & F;
+                }
+                __syncthreads();
+            } else if (want_fail) {
                 if (tid == 0) s_fail = 0;
                 __syncthreads();  // rw complete
                 uint64_t fm = 0;
@@ -1120,35 +1176,34 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
 
 // ---------------------------------------------------------------- LDS-resident min-sum BP
 // Min-sum BP (fp32) for graphs whose messages spill the small-graph LDS budget
-// but whose v2c rows alone fit one CU's 160 KB LDS (config 4: m = 4800 rows of
+// but whose edge slots alone fit one CU's 160 KB LDS (config 4: m = 4800 rows of
 // kMlDRS = 8 floats = 150 KB).  One 1024-thread workgroup per CU decodes one
 // shot at a time with every message on chip:
-//   rows   [m][kMlDRS] f32: v2c messages at (row, CSR position); after the check
-//          pass, slots 0..2 or 4..6 (by bit 3 of the row: rows then spread their
-//          state over all 16 four-bank slots) hold the check's state: m1 and m2
-//          (minimum and second minimum of |v|, counted with multiplicity) carrying
-//          the row parity in their sign bits, and the position of the minimum
+//   rows   [m][kMlDRS] f32: one slot per edge at (row, position); it holds the
+//          edge's v2c message between the variable pass and the check pass and
+//          its c2v message between the check pass and the variable pass
 //   pbuf   two bit arrays of m bits: parity of the hard decision per check,
 //          built by the variable pass with LDS xor atomics (only ones touch it)
-// Thread t owns checks t + 1024 c and variables t + 1024 r.  A variable keeps
-// in registers only its messages' old signs (one bit per edge): with the
-// argmin position in the state, c_k = alpha * ((k's position == argmin) ? m2 :
-// m1) picks the same value as ldpc's leave-one-out minimum (when the minimum is
-// tied, m2 = m1 and every edge gets m1 either way), and the sign is parity ^
-// (v_k <= 0).  Per iteration (3 barriers):
+// Thread t owns checks t + 1024 c and variables t + 1024 r.  Per iteration (2
+// barriers):
 //   A  check pass: syndrome test of the previous iteration's hard decision
-//      (parity bits vs syndrome), then the state of iteration it into slots 0..2
+//      (parity bits vs syndrome); each owned row reads its v2c slots (two
+//      16-B halves), takes m1 / m2 (minimum and second minimum of |v|, counted
+//      with multiplicity), the argmin position and the parity, and writes every
+//      slot's c2v: alpha * (m2 at the argmin, m1 elsewhere) with sign parity ^
+//      (own v2c <= 0) -- ldpc's leave-one-out minimum and sign, bit for bit
+//      (when the minimum is tied m2 = m1, so the argmin's choice is immaterial)
 //   B  barrier-or: all checks satisfied -> converged at it - 1
-//   C  variable pass: gather states, c_k, prefix / suffix sums (ldpc's order),
-//      hard decision, parity xors; new v2c kept in registers
-//   D  barrier (every state read before any row slot is overwritten)
-//   E  scatter v2c into the rows, barrier
+//   C  variable pass: read the c2v slots, prefix / suffix sums (ldpc's order),
+//      hard decision, parity xors, and the new v2c written back into the same
+//      slots at once (a slot is read and written by its own variable only)
+//   D  barrier
 // Finished shots go to the SSF queue in the byte format of the other BP kernels (hard
-// decision, residual, converged bit); ssf_block_kernel runs SSF and finalises.
+// decision, residual, converged bit); ssf_inc_block_kernel runs SSF and finalises.
 // Pad edges (k >= the column's degree, variables j >= n) point at dummy rows
 // past row m (element m * kMlDRS + lane, so no two lanes of a wave write the
-// same address): they gather garbage that the sums mask out and scatter into
-// them, so the loops have no per-edge branches; only real edges xor parity.
+// same address): they read garbage that the sums mask out and write into them,
+// so the loops have no per-edge branches; only real edges xor parity.
 constexpr int kMlThreads = 1024;
 
 constexpr int kMlDummyRows = 64 / kMlDRS;  // pad edges of lane l use element m * kMlDRS + l
@@ -1164,7 +1219,7 @@ template <int VPT>
 __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, DecodeArgs a,
                                                               const uint16_t* __restrict__ etab,
                                                               const float* __restrict__ prior) {
-    static_assert(VPT * kMlDC <= 64, "sign bits");
+    static_assert(VPT * 3 <= 64 && VPT <= 32, "degree and decision bits");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     long long* next = reinterpret_cast<long long*>(smem + 56);
     float* rows = reinterpret_cast<float*>(smem + kCtrl);
@@ -1208,6 +1263,14 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
 #pragma unroll
             for (int h = 0; h < kMlDC / 2; ++h) asm volatile("" : "+v"(ep[r][h]));
     };
+    uint64_t djs = 0;  // 3 bits per owned variable: its degree (real edges come first)
+#pragma unroll
+    for (int r = 0; r < VPT; ++r) {
+        int dj = 0;
+#pragma unroll
+        for (int k = 0; k < kMlDC; ++k) dj += edge(r, k) < pad0;
+        djs |= (uint64_t)dj << (3 * r);
+    }
     uint32_t rdeg = 0;  // 4 bits per owned check (degrees <= 8), checks c < 8
     for (int c = 0; c < ncr && c < 8; ++c) {
         const int i = c * kMlThreads + tid;
@@ -1221,34 +1284,31 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
         if (shot >= a.B) break;
         uint32_t sb = 0;  // syndrome bits of the owned checks
         for (int c = 0; c < ncr; ++c) sb |= (uint32_t)(a.syn[shot * m + c * kMlThreads + tid] & 1) << c;
-        // v2c = prior on every edge; old signs
-        uint64_t sg = 0;  // bit r * kMlDC + k: v2c message k of variable r is <= 0
+        // v2c = prior on every edge
         opaque_edges();
 #pragma unroll
         for (int r = 0; r < VPT; ++r)
 #pragma unroll
-            for (int k = 0; k < kMlDC; ++k) {
-                rows[edge(r, k)] = L[r];
-                sg |= (uint64_t)(L[r] <= 0.0f) << (r * kMlDC + k);
-            }
+            for (int k = 0; k < kMlDC; ++k) rows[edge(r, k)] = L[r];
         __syncthreads();
 
         uint32_t xb = 0, bad = 0;  // hard decisions (bit r), failing owned checks (bit c)
         bool conv = false;
         int it = 1;
         for (;; ++it) {
-            // ---- A: test of iteration it - 1, then the check state of iteration it
+            // ---- A: test of iteration it - 1, then the c2v messages of iteration it
             const uint32_t* pprev = pb0 + ((it - 1) & 1) * pbw;
             uint32_t* pcur = pb0 + (it & 1) * pbw;
             const bool work = it <= a.max_iter;
+            const float alpha = alpha_at<float>(it, a.ms_scaling);
             bad = 0;
             for (int c = 0; c < ncr; ++c) {
                 const int i = c * kMlThreads + tid;
                 if (it > 1) bad |= (((pprev[i >> 5] >> (i & 31)) ^ (sb >> c)) & 1u) << c;
                 if (work) {
                     const int deg = c < 8 ? (int)((rdeg >> (4 * c)) & 15u) : (g.row_ptr[i + 1] - g.row_ptr[i]);
-                    // state half of the row first (so = 4 * bit 3 of the row: 16
-                    // consecutive rows then start in 16 distinct 4-bank slots);
+                    // the row's halves in swizzled order (so = 4 * bit 3 of the row:
+                    // 16 consecutive rows then start in 16 distinct 4-bank slots);
                     // loaded element u sits at row position (u + so) & 7
                     const int so = ((i >> 3) & 1) << 2;
                     float v[kMlDRS];
@@ -1271,12 +1331,19 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                         m1 = med3(av, m1, -Big<float>::v);
                         par ^= vt <= 0.0f;
                     }
-                    float4 st;
-                    st.x = par ? -m1 : m1;
-                    st.y = par ? -m2 : m2;
-                    st.z = __int_as_float(amin);
-                    st.w = 0.0f;
-                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + so) = st;
+                    // c2v of every position, in place of its v2c: alpha times the
+                    // leave-one-out minimum (m2 at the argmin, m1 elsewhere), sign =
+                    // syndrome ^ the other edges' signs = par ^ (own v2c <= 0)
+                    const float y1 = m1 * alpha, y2 = m2 * alpha;
+                    float o[kMlDRS];
+#pragma unroll
+                    for (int u = 0; u < kMlDRS; ++u) {
+                        const int t = (u + so) & (kMlDRS - 1);
+                        const float y = t == amin ? y2 : y1;
+                        o[u] = (par ^ (uint32_t)(v[u] <= 0.0f)) ? -y : y;
+                    }
+                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + so) = make_float4(o[0], o[1], o[2], o[3]);
+                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + (so ^ 4)) = make_float4(o[4], o[5], o[6], o[7]);
                 }
             }
             if (work)
@@ -1295,26 +1362,25 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                 break;
             }
             if (!work) break;
-            // ---- C: variable pass (new messages stay in registers until E)
-            const float alpha = alpha_at<float>(it, a.ms_scaling);
+            // ---- C: variable pass.  Each edge's slot is read and rewritten by its
+            // own variable only (c2v in, new v2c out), so no barrier separates them
             opaque_edges();
-            float out[VPT][kMlDC];
             xb = 0;
+            // software-pipelined by one variable: the next variable's slots are
+            // read before this one's arithmetic (distinct slots, so the order
+            // against this variable's writes is immaterial)
+            float cn[kMlDC];
+#pragma unroll
+            for (int k = 0; k < kMlDC; ++k) cn[k] = rows[edge(0, k)];
 #pragma unroll
             for (int r = 0; r < VPT; ++r) {
-                int dj = 0;  // degree: real edges come first, pads point past the rows
-#pragma unroll
-                for (int k = 0; k < kMlDC; ++k) dj += edge(r, k) < pad0;
+                const int dj = (int)((djs >> (3 * r)) & 7u);  // degree: real edges come first
                 float c[kMlDC];
 #pragma unroll
-                for (int k = 0; k < kMlDC; ++k) {
-                    const uint32_t e = edge(r, k);
-                    // state slots of row e / 8: the half selected by bit 3 of the row (see A)
-                    const float4 st = *reinterpret_cast<const float4*>(rows + ((e & ~(uint32_t)(kMlDRS - 1)) | ((e >> 4) & 4u)));
-                    const float y = ((int)(e & (kMlDRS - 1)) == __float_as_int(st.z)) ? st.y : st.x;
-                    const float yk = y * alpha;
-                    c[k] = ((sg >> (r * kMlDC + k)) & 1) ? -yk : yk;
-                }
+                for (int k = 0; k < kMlDC; ++k) c[k] = cn[k];
+                if (r + 1 < VPT)
+#pragma unroll
+                    for (int k = 0; k < kMlDC; ++k) cn[k] = rows[edge(r + 1, k)];
                 // ldpc's order: prefix sums from the prior, then each outgoing
                 // message = prefix + (sum of the later edges, accumulated from the end)
                 float pre[kMlDC];
@@ -1333,9 +1399,7 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                     const float o = started ? pre[k] + suf : pre[k];
                     suf = started ? suf + c[k] : c[k];
                     started = started || k < dj;
-                    out[r][k] = o;
-                    const uint64_t bit = 1ull << (r * kMlDC + k);
-                    sg = (o <= 0.0f) ? (sg | bit) : (sg & ~bit);
+                    rows[edge(r, k)] = o;
                 }
                 if (x) {
 #pragma unroll
@@ -1344,17 +1408,10 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                         if (k < dj) atomicXor(&pcur[i >> 5], 1u << (i & 31));
                     }
                 }
-                // one variable's gathers in flight at a time (otherwise the
+                // two variables' reads in flight at most (otherwise the
                 // scheduler hoists all of them and spills)
                 __builtin_amdgcn_sched_barrier(0);
             }
-            __syncthreads();
-            // ---- E: scatter
-            opaque_edges();
-#pragma unroll
-            for (int r = 0; r < VPT; ++r)
-#pragma unroll
-                for (int k = 0; k < kMlDC; ++k) rows[edge(r, k)] = out[r][k];
             __syncthreads();
         }
         // ---- queue the shot: hard decision, residual syndrome, converged bit

@@ -153,6 +153,13 @@ struct DevGraph {
     const int32_t* lz_ptr;        // [k+1]
     const int32_t* lz_idx;        // [nnz]
     int lz_sparse;
+    // the same logicals by qubit: word t of qubit q holds bit r % 32 of logical
+    // r = 32 t + (r % 32) (nullptr when n_data * lz_tw words exceed 64 MB).  The
+    // workgroup finalizes test a residual through it: only the residual's ones
+    // read their qubit's lz_tw words, so a decoded shot (residual zero or a
+    // stabilizer) costs a few words instead of k * lz_words
+    const uint32_t* lz_t;         // [n_data][lz_tw]
+    int lz_tw;
     // per-handle kernel choices (qd_graph_set_option, QD_OPT_* in include/qdec.h;
     // defaults from default_options): the launchers read these, never the
     // environment
