@@ -86,6 +86,12 @@ SIGNATURES = {
     "qd_graph_ssf_tables_copy": (_i32, [_p, _p, _p, _p, _p, C.POINTER(_i32), C.POINTER(_i32)]),
     "qd_graph_queue_layout": (_i32, [_p, _i64, _p]),
     "qd_graph_it1_tables_copy": (_i32, [_p, _i32, _p, _p, C.POINTER(_i32)]),
+    "qd_graph_hgp_info": (_i32, [_p, _p]),
+    "qd_graph_hgp_set_slots": (_i32, [_p, _i32]),
+    "qd_graph_hgp_source": (_i64, [_p, C.c_char_p, _i64]),
+    "qd_graph_hgp_compile": (_i32, [_p]),
+    "qd_graph_hgp_replace_source": (_i32, [_p, C.c_char_p]),
+    "qd_graph_hgp_decode_bp": (_i32, [_p, _i64, _p, _p, _p, _p, _i32, C.c_double, _p]),
     "qd_gf2_rref": (_i64, [_p, _i64, _i64, _i64, _p, _i32]),
     "qd_gf2_extend_basis": (_i64, [_p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64]),
 }

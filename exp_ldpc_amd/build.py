@@ -19,7 +19,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libqdec_hip.so")
-SOURCES = ["qdec_abi.cpp", "qdec_osd.cpp", "qdec_gf2.cpp", "qdec_bp.hip", "qdec_bp_block.hip", "qdec_sample.hip", "qdec_osd.hip"]
+SOURCES = ["qdec_abi.cpp", "qdec_osd.cpp", "qdec_gf2.cpp", "qdec_hgp.cpp", "qdec_bp.hip", "qdec_bp_block.hip",
+           "qdec_sample.hip", "qdec_osd.hip"]
+# device source compiled at run time (hipRTC, per hypergraph-product code): embedded
+# into the library as a string literal (build/gen/qdec_hgp_src.inc)
+RTC_SOURCES = ["qdec_hgp_kernel.hip"]
 HEADERS = [os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.h"))] + ["../../include/qdec.h"]
 ARCH = os.environ.get("QDEC_OFFLOAD_ARCH", "gfx950")
 
@@ -41,7 +45,7 @@ def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + RTC_SOURCES] + [__file__]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
@@ -68,7 +72,14 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
     extra = (["-DQDEC_STAMPS"] if stamps else []) + [f"-D{d}" for d in defines] + list(flags)
     objdir = os.path.join(os.path.dirname(HERE), "build", "obj" + suffix)
     os.makedirs(objdir, exist_ok=True)
-    cflags = [f for f in FLAGS if f != "-shared"]
+    gendir = os.path.join(os.path.dirname(HERE), "build", "gen")
+    os.makedirs(gendir, exist_ok=True)
+    for src in RTC_SOURCES:
+        text = open(os.path.join(CSRC, src)).read()
+        assert ")QDEC_RTC\"" not in text
+        with open(os.path.join(gendir, src.replace("_kernel.hip", "_src.inc")), "w") as fh:
+            fh.write('R"QDEC_RTC(' + text + ')QDEC_RTC"\n')
+    cflags = [f for f in FLAGS if f != "-shared"] + ["-I", gendir]
 
     def compile_one(src):
         obj = os.path.join(objdir, src + ".o")
@@ -86,7 +97,8 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = lib + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *link_flags, "-o", tmp, *objs]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *link_flags, "-o", tmp, *objs,
+           "-lhiprtc"]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-6000:]}")

@@ -127,6 +127,9 @@ struct qd_graph {
     std::string last_bp, last_ssf, last_pre;
     // qd_graph_create_host: tables only, no device, no stream; decodes refuse it
     bool host_only = false;
+    // hypergraph-product kernel (qd_graph_hgp_*): plan once per graph
+    HgpPlan* hgp = nullptr;
+    bool hgp_tried = false;
 };
 
 namespace {
@@ -1038,11 +1041,109 @@ int qd_graph_table_digest(const qd_graph* G, uint64_t* digest, int64_t* bytes) {
     });
 }
 
+static HgpPlan* hgp_plan_of(qd_graph* G) {
+    if (!G->hgp_tried) {
+        G->hgp = hgp_plan_create(G->dg.m, G->dg.n, G->row_ptr, G->col_idx);
+        G->hgp_tried = true;
+    }
+    return G->hgp;
+}
+
+int qd_graph_hgp_set_slots(qd_graph* G, int32_t slots) {
+    return guarded([&] {
+        check_graph(G);
+        if (slots < 0 || slots > 64) throw Fail(-95, "slots out of range");
+        if (!G->host_only) set_device(G);
+        if (G->stream) hip_check(hipStreamSynchronize(G->stream), "hipStreamSynchronize");
+        hgp_plan_destroy(G->hgp);
+        G->hgp = hgp_plan_create(G->dg.m, G->dg.n, G->row_ptr, G->col_idx, slots);
+        G->hgp_tried = true;
+    });
+}
+
+int qd_graph_hgp_info(qd_graph* G, int32_t* out8) {
+    int rc = 0;
+    const int e = guarded([&] {
+        check_graph(G);
+        HgpPlan* P = hgp_plan_of(G);
+        rc = P ? 1 : 0;
+        if (P && out8) hgp_plan_info(P, out8);
+    });
+    return e ? e : rc;
+}
+
+int64_t qd_graph_hgp_source(qd_graph* G, char* buf, int64_t cap) {
+    int64_t len = 0;
+    const int e = guarded([&] {
+        check_graph(G);
+        HgpPlan* P = hgp_plan_of(G);
+        if (!P) throw Fail(-90, "not a hypergraph-product check matrix");
+        const std::string& s = hgp_plan_source(P);
+        len = (int64_t)s.size();
+        if (buf && cap > 0) {
+            const size_t k = std::min<size_t>(s.size(), (size_t)cap - 1);
+            std::memcpy(buf, s.data(), k);
+            buf[k] = 0;
+        }
+    });
+    return e ? e : len;
+}
+
+int qd_graph_hgp_replace_source(qd_graph* G, const char* src) {
+    return guarded([&] {
+        check_graph(G);
+        HgpPlan* P = hgp_plan_of(G);
+        if (!P || !src) throw Fail(-90, "not a hypergraph-product check matrix");
+        if (G->stream) hip_check(hipStreamSynchronize(G->stream), "hipStreamSynchronize");
+        hgp_plan_replace_source(P, src);
+    });
+}
+
+int qd_graph_hgp_compile(qd_graph* G) {
+    return guarded([&] {
+        check_graph(G);
+        HgpPlan* P = hgp_plan_of(G);
+        if (!P) throw Fail(-90, "not a hypergraph-product check matrix");
+        std::string log;
+        if (hgp_plan_compile(P, "gfx950", &log) != 0) throw Fail(-91, "HGP kernel compile failed: " + log);
+    });
+}
+
+int qd_graph_hgp_decode_bp(qd_graph* G, int64_t B, const uint8_t* syn, uint8_t* x_out, int32_t* iters,
+                           uint8_t* status, int32_t max_iter, double ms_scaling, void* stream) {
+    return guarded([&] {
+        check_graph(G);
+        if (G->host_only) throw Fail(-2, "host-only graph handle");
+        set_device(G);
+        HgpPlan* P = hgp_plan_of(G);
+        if (!P) throw Fail(-90, "not a hypergraph-product check matrix");
+        if (!G->has_priors) throw Fail(-51, "priors not set");
+        if (B < 0 || (B > 0 && !syn) || max_iter < 1) throw Fail(-92, "invalid HGP decode arguments");
+        if (hgp_plan_load(P, G->num_cus) != 0) throw Fail(-93, "HGP kernel load failed");
+        if (!G->ctl) hip_check(hipMalloc(&G->ctl, 256), "hipMalloc control block");
+        if (B == 0) return;
+        HgpBpArgs a{};
+        a.syn = syn;
+        a.prior = static_cast<const double*>(G->dg.prior[QD_MIN_SUM][QD_F64]);
+        a.x_out = x_out;
+        a.iters = iters;
+        a.status = status;
+        a.counter = static_cast<unsigned long long*>(G->ctl) + 1;
+        a.B = B;
+        a.max_iter = max_iter;
+        a.ms_scaling = ms_scaling;
+        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : G->stream;
+        if (hgp_launch_bp(P, a, st) != 0) throw Fail(-94, "HGP kernel launch failed");
+        hip_check(hipGetLastError(), "HGP kernel");
+    });
+}
+
 int qd_graph_destroy(qd_graph* g) {
     return guarded([&] {
         if (!g) return;
         if (g->host_only) {
             for (DevArena* a : {&g->arena, &g->flip_arena, &g->lz_arena, &g->prior_arena}) a->release();
+            hgp_plan_destroy(g->hgp);
             delete g;
             return;
         }
@@ -1059,6 +1160,7 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->qws) (void)hipFree(g->qws);
         if (g->mws) (void)hipFree(g->mws);
         if (g->ctl) (void)hipFree(g->ctl);
+        hgp_plan_destroy(g->hgp);
         free_timing(g);
         if (g->stream) (void)hipStreamDestroy(g->stream);
         delete g;

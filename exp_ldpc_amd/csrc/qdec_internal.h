@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 namespace qdec {
 
@@ -329,5 +330,31 @@ int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint
                           uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
                           uint8_t* syn, uint8_t* readout, int num_cus, hipStream_t stream);
 int launch_count_flags(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, hipStream_t stream);
+
+// ---------------------------------------------------------------- HGP kernel
+// Hypergraph-product codes get their own f64 min-sum BP kernel, generated and
+// compiled per code with hipRTC (qdec_hgp.cpp, qdec_hgp_kernel.hip).
+struct HgpPlan;
+struct HgpBpArgs {  // the kernel's HgArgs, field for field
+    const uint8_t* syn;           // [B][m]
+    const double* prior;          // [n] min-sum prior per column
+    uint8_t* x_out;               // [B][n] or null
+    int32_t* iters;               // [B] or null
+    uint8_t* status;              // [B] or null (bit 0: BP converged)
+    unsigned long long* counter;  // shot counter (zeroed by hgp_launch_bp)
+    int64_t B;
+    int32_t max_iter;
+    double ms_scaling;
+};
+// nullptr unless H = [I_a0 (x) B | A (x) I_b0] within the kernel's limits
+// slots: shot slots per workgroup (0: the plan's choice)
+HgpPlan* hgp_plan_create(int m, int n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int slots = 0);
+void hgp_plan_destroy(HgpPlan* P);
+const std::string& hgp_plan_source(const HgpPlan* P);
+void hgp_plan_replace_source(HgpPlan* P, const std::string& src);  // development
+int hgp_plan_compile(HgpPlan* P, const char* arch, std::string* log);  // hipRTC (no device needed)
+int hgp_plan_load(HgpPlan* P, int num_cus);                              // compile + load on the current device
+int hgp_launch_bp(HgpPlan* P, const HgpBpArgs& a, hipStream_t stream);
+void hgp_plan_info(const HgpPlan* P, int* out8);  // a0 a1 b0 b1 S WL WR per_cu
 
 }  // namespace qdec

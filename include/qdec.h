@@ -289,6 +289,29 @@ int qd_graph_it1_tables_copy(const qd_graph* g, int32_t precision, uint16_t* lut
 int qd_graph_ssf_tables_copy(const qd_graph* g, uint32_t* lut, uint32_t* off, uint32_t* lcw, uint32_t* tog,
                              int32_t* g_pad, int32_t* m_pad);
 
+/* Hypergraph-product kernel (qdec_hgp.cpp, qdec_hgp_kernel.hip).  When H =
+ * [I_a0 (x) B | A (x) I_b0] (the Z checks of hgp.py homological_product, e.g.
+ * biregular_hgp, reference python/qldpc/hypergraph_product_code.py:7-35), the
+ * library generates an f64 min-sum BP kernel with B's and A's Tanner graphs as
+ * compile-time tables and compiles it with hipRTC.  qd_graph_hgp_info: 1 and
+ * out8 = {a0, a1, b0, b1, shot slots per workgroup, left waves, right waves,
+ * workgroups per CU (0 before the first decode)} for such a graph, 0 otherwise.
+ * qd_graph_hgp_source: the generated source (its length; copied into buf).
+ * qd_graph_hgp_compile: compile only (no device needed).  No reference
+ * counterpart (the reference decodes with ldpc's generic BpDecoder). */
+int qd_graph_hgp_info(qd_graph* g, int32_t* out8);
+/* Re-plan with `slots` shot slots per workgroup (0: the library's choice). */
+int qd_graph_hgp_set_slots(qd_graph* g, int32_t slots);
+int64_t qd_graph_hgp_source(qd_graph* g, char* buf, int64_t cap);
+int qd_graph_hgp_compile(qd_graph* g);
+/* Development: replace the generated source (kernel debugging, tools/dev). */
+int qd_graph_hgp_replace_source(qd_graph* g, const char* src);
+/* BP only (f64 min-sum, ldpc v1 semantics as qd_decode_batch_device with
+ * method QD_MIN_SUM, precision QD_F64, no SSF): device buffers syn [B][m],
+ * x_out [B][n] (or null), iters [B], status [B] (bit 0: converged). */
+int qd_graph_hgp_decode_bp(qd_graph* g, int64_t B, const uint8_t* syn, uint8_t* x_out, int32_t* iters,
+                           uint8_t* status, int32_t max_iter, double ms_scaling, void* stream);
+
 /* Device-side sum of a uint8 flag array (failure / status counts) into *out
  * (device int64, accumulated: caller zeroes it).  `mask` selects bits. */
 int qd_count_flags_device(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, void* stream);

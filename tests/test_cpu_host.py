@@ -547,3 +547,60 @@ def test_kernel_options_are_handle_state_not_environment(code225):
     assert srcs
     for f in srcs:
         assert not re.search(r"\bgetenv\s*\(", open(f).read()), f
+
+
+def test_hgp_kernel_plan_and_rtc_compile(code225):
+    """The hypergraph-product kernel (qdec_hgp.cpp): the n = 225 code's Z checks
+    factor as [I_12 (x) B | A (x) I_9] with B = A^T (hgp.py homological_product),
+    the generated source carries B's and A's edge tables, and hipRTC compiles it
+    for gfx950 without a device.  A random matrix, and the same code with two
+    columns swapped, are not recognised."""
+    import ctypes as C
+
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    hz = sp.csr_matrix(code225.checks.z)
+    h, _, _ = _host_graph(lib, hz, probs=0.01)
+    info = (C.c_int32 * 8)()
+    assert lib.qd_graph_hgp_info(h, info) == 1
+    a0, a1, b0, b1, S, WL, WR, _ = list(info)
+    assert (a0, a1, b0, b1) == (12, 9, 9, 12)
+    assert S >= 1 and WL == (S * a0 + 63) // 64 and WR == (S * b0 + 63) // 64 and WL + WR <= 16
+    L = lib.qd_graph_hgp_source(h, None, 0)
+    assert L > 0
+    buf = C.create_string_buffer(int(L) + 1)
+    assert lib.qd_graph_hgp_source(h, buf, L + 1) == L
+    src = buf.value.decode()
+    # the factors, as the generator wrote them, rebuild the matrix exactly
+    def table(name):
+        body = src.split(f"k{name}[")[1].split("{", 1)[1].split("}", 1)[0]
+        return [int(t.rstrip("ul")) for t in body.split(",")]
+    Brp, Bce, Aer = table("Brp"), table("Bce"), table("Aer")
+    assert Brp[-1] == len(Bce) == 36 and len(Aer) == 36
+    A = np.zeros((a0, a1), np.uint8)
+    B = np.zeros((b0, b1), np.uint8)
+    Arp, Bcp = table("Arp"), table("Bcp")
+    Arm, Brm = table("Arm"), table("Brm")
+    for x in range(a0):
+        for w in range(a1):
+            A[x, w] = (Arm[x] >> w) & 1
+    for y in range(b0):
+        for z in range(b1):
+            B[y, z] = (Brm[y] >> z) & 1
+    H2 = sp.hstack([sp.kron(sp.identity(a0), B), sp.kron(A, sp.identity(b0))]).toarray() % 2
+    assert np.array_equal(H2, hz.toarray() % 2)
+    assert np.array_equal(A.T, B)  # biregular_hgp: B = A^T
+    assert [sum(Arm[x] >> w & 1 for w in range(a1)) for x in range(a0)] == list(np.diff(Arp))
+    _abi.check(lib.qd_graph_hgp_compile(h), "hgp compile")  # hipRTC, no device
+    lib.qd_graph_destroy(h)
+    # not hypergraph products
+    rng = np.random.default_rng(3)
+    R = sp.csr_matrix((rng.random((108, 225)) < 0.03).astype(np.uint8))
+    h2, _, _ = _host_graph(lib, R, probs=0.01)
+    assert lib.qd_graph_hgp_info(h2, info) == 0
+    lib.qd_graph_destroy(h2)
+    P = hz.toarray()
+    P[:, [0, 150]] = P[:, [150, 0]]
+    h3, _, _ = _host_graph(lib, P, probs=0.01)
+    assert lib.qd_graph_hgp_info(h3, info) == 0
+    lib.qd_graph_destroy(h3)
