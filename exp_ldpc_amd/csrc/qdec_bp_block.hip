@@ -1307,10 +1307,12 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                 if (it > 1) bad |= (((pprev[i >> 5] >> (i & 31)) ^ (sb >> c)) & 1u) << c;
                 if (work) {
                     const int deg = c < 8 ? (int)((rdeg >> (4 * c)) & 15u) : (g.row_ptr[i + 1] - g.row_ptr[i]);
-                    // the row's halves in swizzled order (so = 4 * bit 3 of the row:
-                    // 16 consecutive rows then start in 16 distinct 4-bank slots);
-                    // loaded element u sits at row position (u + so) & 7
-                    const int so = ((i >> 3) & 1) << 2;
+                    // the row's halves in swizzled order (so = 4 * bit 4 of the row):
+                    // the 16-B reads of a 16-lane group (banks a/4 mod 64) and the
+                    // 16-B writes of an 8-lane group (banks a/4 mod 32) then land in
+                    // distinct 4-bank slots; loaded element u sits at row position
+                    // u ^ so
+                    const int so = ((i >> 4) & 1) << 2;
                     float v[kMlDRS];
                     {
                         const float4 h0 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + so);
@@ -1318,29 +1320,32 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
                         v[0] = h0.x, v[1] = h0.y, v[2] = h0.z, v[3] = h0.w;
                         v[4] = h1.x, v[5] = h1.y, v[6] = h1.z, v[7] = h1.w;
                     }
+                    // sign test by bits: bit 31 of bits(v) - 1 is (v <= 0) for every v
+                    // but -0, and a v2c message is never -0 (the prior is not, and a
+                    // sum is -0 only when both terms are)
                     float m1 = Big<float>::v, m2 = Big<float>::v;
-                    int amin = 0;
-                    uint32_t par = (sb >> c) & 1u;
+                    int au = 0;  // element index of the argmin
+                    uint32_t sx = ((sb >> c) & 1u) << 31;
+                    uint32_t sg[kMlDRS];
 #pragma unroll
                     for (int u = 0; u < kMlDRS; ++u) {
-                        const int t = (u + so) & (kMlDRS - 1);
-                        const float vt = t < deg ? v[u] : Big<float>::v;
+                        const float vt = (u ^ so) < deg ? v[u] : Big<float>::v;
                         const float av = fabsf(vt);
-                        amin = av < m1 ? t : amin;
+                        au = av < m1 ? u : au;
                         m2 = med3(av, m1, m2);
                         m1 = med3(av, m1, -Big<float>::v);
-                        par ^= vt <= 0.0f;
+                        sg[u] = (uint32_t)__float_as_int(vt) - 1u;
+                        sx ^= sg[u];
                     }
                     // c2v of every position, in place of its v2c: alpha times the
                     // leave-one-out minimum (m2 at the argmin, m1 elsewhere), sign =
-                    // syndrome ^ the other edges' signs = par ^ (own v2c <= 0)
+                    // syndrome ^ the other edges' signs = bit 31 of sx ^ sg[u]
                     const float y1 = m1 * alpha, y2 = m2 * alpha;
                     float o[kMlDRS];
 #pragma unroll
                     for (int u = 0; u < kMlDRS; ++u) {
-                        const int t = (u + so) & (kMlDRS - 1);
-                        const float y = t == amin ? y2 : y1;
-                        o[u] = (par ^ (uint32_t)(v[u] <= 0.0f)) ? -y : y;
+                        const float y = u == au ? y2 : y1;
+                        o[u] = __uint_as_float(__float_as_uint(y) ^ ((sg[u] ^ sx) & 0x80000000u));
                     }
                     *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + so) = make_float4(o[0], o[1], o[2], o[3]);
                     *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + (so ^ 4)) = make_float4(o[4], o[5], o[6], o[7]);
