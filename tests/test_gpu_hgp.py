@@ -71,3 +71,23 @@ def test_hgp_kernel_ms_scaling_and_short_runs(gpu_available, oracle_lib, code225
                                 want_llr=False)
         assert np.array_equal(it, ref["iters"]) and np.array_equal(x, ref["x"])
         assert np.array_equal(st & 1, ref["status"] & 1)
+
+
+def test_hgp_kernel_zero_priors(gpu_available, oracle_lib, code225):
+    """Columns with p = 0.5 (prior LLR +0) and p > 0.5: zero and negative
+    messages reach the partial states, exercising the kernel's rare exact-parity
+    branch and the +0 flag of the merged m2 (MsCore's zero rule)."""
+    import torch
+
+    from exp_ldpc_amd.decoder import Decoder
+    hz = sp.csr_matrix(code225.checks.z)
+    rng = np.random.default_rng(11)
+    B = 1000
+    e = (rng.random((B, 225)) < 0.03).astype(np.uint8)
+    syn = np.ascontiguousarray(((hz @ e.T).T % 2).astype(np.uint8))
+    probs = rng.choice([0.5, 0.6, 0.02, 0.02, 0.05], 225)
+    dec = Decoder(hz, probs, method="ms", precision="f64", max_iter=25, device=0)
+    x, it, st = _hgp_decode(dec, torch.from_numpy(syn).to("cuda:0"), B, 25)
+    ref = oracle_lib.decode(hz, probs, syn, method="ms", precision="f64", max_iter=25, want_llr=False)
+    assert np.array_equal(it, ref["iters"]) and np.array_equal(x, ref["x"])
+    assert np.array_equal(st & 1, ref["status"] & 1)

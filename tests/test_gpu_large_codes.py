@@ -229,6 +229,30 @@ def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatc
         _decode_both(oracle_lib, H, probs, syn, max_iter=30, ms_scaling=scaling)
 
 
+def test_lds_kernel_zero_and_negative_priors(gpu_available, oracle_lib, monkeypatch):
+    """bp_ms_lds_kernel's sign-bit check pass on messages that are exactly zero
+    (columns with p = 0.5: prior LLR +0, so +0 v2c messages and -0 c2v ones)
+    and negative (p > 0.5), beside ordinary columns: x / iterations / status
+    bit-exact against the oracle's compares."""
+    from exp_ldpc_amd.codes import make_check_matrix
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
+    rng = np.random.default_rng(5)
+    m, n = 900, 1600
+    rows, colcount = [], np.zeros(n, int)
+    for i in range(m):
+        d = int(rng.integers(2, 9))
+        cand = [j for j in rng.permutation(n) if colcount[j] < 4][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    H = make_check_matrix(rows, n)
+    e = (rng.random((300, n)) < 0.03).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.choice([0.5, 0.5, 0.6, 0.02, 0.05, 0.01], n)
+    for scaling in (0.0, 0.625):
+        _decode_both(oracle_lib, H, probs, syn, max_iter=20, ms_scaling=scaling)
+
+
 @pytest.mark.parametrize("scoring", ["auto", "scan"])
 def test_hgp10k_ssf_table_scoring_parity(gpu_available, oracle_lib, hgp10k, scoring, monkeypatch):
     """The incremental workgroup SSF kernel scores generators by table lookup
