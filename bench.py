@@ -17,7 +17,11 @@ Phases (rank 0 prints ONE JSON line):
      HIP streams (default 9: every point on its own stream; measured 79 vs 76 M
      f64 shots/s at 5), so kernels of independent points fill each other's tails;
      f64 wave kernels run at 12 waves per CU here (--wave-occupancy; a lone
-     decode keeps 8, its own optimum)
+     decode keeps 8, its own optimum); each point's steps run back to back on
+     its stream and the streams join once, at the end of the timed region
+     (--step-join end; joining them every step left each step's slowest point
+     running alone at its end: 112.0 / 113.3 vs 116.9 / 117.3 M f64 shots/s,
+     profiles/r05q/)
      (--schedule pipeline: every BP kernel on one stream and every SSF kernel on
      a second one behind an event -- measured slower: the persistent BP kernel
      fills every CU, so SSF only runs in BP's tail, which it cannot fill because
@@ -574,20 +578,23 @@ class Run:
                                        ssf_steps=self.ssf_steps[s, pi],
                                        **({} if self.fake else {"stream": streams[0].cuda_stream}))
             return
-        ev = torch.cuda.Event()
-        ev.record(streams[0])
-        for st in streams[1:]:
-            st.wait_event(ev)
+        join = self.args.step_join == "step"
+        if join:
+            ev = torch.cuda.Event()
+            ev.record(streams[0])
+            for st in streams[1:]:
+                st.wait_event(ev)
         order = range(len(self.ps)) if self.args.point_order == "asc" else range(len(self.ps) - 1, -1, -1)
         for j, pi in enumerate(order):
             st = streams[j % len(streams)]
             decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                    status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi],
                                    stream=st.cuda_stream)
-        for st in streams[1:]:
-            e2 = torch.cuda.Event()
-            e2.record(st)
-            streams[0].wait_event(e2)
+        if join:
+            for st in streams[1:]:
+                e2 = torch.cuda.Event()
+                e2.record(st)
+                streams[0].wait_event(e2)
 
     def timed(self, decs, steps, streams, sampler=None, warm=True):
         """Run the warmup steps (untimed, unless warm=False), then `steps` timed
@@ -641,6 +648,9 @@ def main():
     ap.add_argument("--wave-occupancy", type=int, default=-1,
                     help="waves per CU of the wave BP kernels in the overlapped phases (qd_graph_set_wave_occupancy); "
                          "-1 = 12 for f64 when the points share the chip over several streams, else the default")
+    ap.add_argument("--step-join", default="end", choices=["step", "end"],
+                    help="streams schedule: join every point's stream at the end of each step (step) or only at the "
+                         "end of the timed region (end: each point's steps run back to back on its stream)")
     ap.add_argument("--point-order", default="asc", choices=["asc", "desc"],
                     help="launch order of the sweep points in the overlapped phases (desc: highest p first)")
     ap.add_argument("--iso-steps", type=int, default=2, help="isolated (one-stream) steps timing each kernel")
@@ -834,7 +844,8 @@ def main():
                                    "alpha_t=1-2^-t + SSF (Hx flip sets) + fused logical check",
                        "shots_per_point_per_step_per_gpu": args.batch, "global_batch": args.batch * P * world,
                        "parallelism": f"shot-sharded x{world}, no collective",
-                       "schedule": args.schedule if args.schedule == "pipeline" else f"{args.streams} streams",
+                       "schedule": args.schedule if args.schedule == "pipeline" else
+                       f"{args.streams} streams, joined {'every step' if args.step_join == 'step' else 'at the end'}",
                        "wave_waves_per_cu": {k: (v or "default") for k, v in occ.items()}},
         }
         if variant:
