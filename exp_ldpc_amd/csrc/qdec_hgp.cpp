@@ -130,13 +130,11 @@ HgpPlan* hgp_plan_create(int m, int n, const std::vector<int32_t>& rp, const std
         delete P;
         return nullptr;
     }
-    // register budget: v2c messages of one copy, qubit masks in 32 bits
+    // register budget: a copy's v2c messages (<= 48 edges) and decision / parity
+    // masks in 32 bits (<= 32 qubits and checks per copy)
     const size_t eA = [&] { size_t s = 0; for (auto& r : P->A) s += r.size(); return s; }();
     const size_t eB = [&] { size_t s = 0; for (auto& r : P->B) s += r.size(); return s; }();
-    int maxdeg = 0;
-    for (auto& r : P->A) maxdeg = std::max(maxdeg, (int)r.size());
-    for (auto& r : P->B) maxdeg = std::max(maxdeg, (int)r.size());
-    if (eA > 48 || eB > 48 || P->a1 > 32 || P->b1 > 32 || P->a0 > 32 || P->b0 > 32 || P->a0 > 64 || P->b0 > 64) {
+    if (eA > 48 || eB > 48 || P->a1 > 32 || P->b1 > 32 || P->a0 > 32 || P->b0 > 32) {
         delete P;
         return nullptr;
     }
@@ -164,7 +162,6 @@ HgpPlan* hgp_plan_create(int m, int n, const std::vector<int32_t>& rp, const std
       << P->b1 << "\n#define HG_S " << P->S << "\n#define HG_WL " << P->WL << "\n#define HG_WR " << P->WR << "\n";
     emit_tables(o, "B", P->B, P->b1);
     emit_tables(o, "A", P->A, P->a1);
-    (void)maxdeg;
     P->src = o.str() + kHgpKernelSrc;
     return P;
 }
