@@ -1433,6 +1433,282 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
     }
 }
 
+// ---------------------------------------------------------------- LDS-resident min-sum BP, f64
+// bp_ms_lds_kernel's one-shot-per-CU scheme at ldpc's precision.  The f64 edge
+// slots of config 4 (33,600 x 8 B) do not fit the 160 KB LDS, so no message is
+// kept there: each variable thread keeps the v2c messages it sent last
+// iteration in registers, and the check side is reduced to its min-sum state,
+// built by LDS atomics on the IEEE bit patterns (|v| >= +0 orders like an
+// unsigned integer, so ds_min_u64 is the exact minimum):
+//   st[b][i]  (m1, m2) as u64 bits: minimum and second minimum of |v| over the
+//             row, with multiplicity (a repeated minimum gives m2 = m1)
+//   parw[b]   per check: syndrome ^ parity of (v <= 0) over the row
+//   tiew[b]   per check: "an edge with |v| == m1 was seen" (the second such edge
+//             sets m2 = m1)
+//   hdw[b]    per check: parity of the hard decision (the syndrome test)
+// Buffers alternate by iteration parity b = it & 1.  Per iteration (2 barriers):
+//   D  variable pass: c2v of edge (i, v) = alpha * (|v| == m1 ? m2 : m1) with
+//      sign parw ^ (v <= 0) -- ldpc's leave-one-out minimum and sign, the same
+//      selection as MsCore's and the f32 kernel's -- then ldpc's prefix / suffix
+//      sums, the hard decision (xor into hdw[b]), and the new v2c messages'
+//      atomics into buffer b ^ 1: ds_min_u64 on m1, xor of the sign parity
+//   B  syndrome test of hdw[b] (a flag per wave); second pass of the new
+//      messages on buffer b ^ 1 (|v| == m1: claim the tie bit, a second claimer
+//      sets m2 = m1; |v| > m1: ds_min_u64 on m2); buffer b reset for
+//      iteration it + 2 (every read of it is behind the barrier)
+// A v2c message is never -0 (see bp_ms_lds_kernel), so (bits(v) - 1) >> 63 is
+// ldpc's (v <= 0).  Finished shots are queued like bp_ms_lds_kernel's.
+constexpr int kM64Threads = 1024;
+
+__host__ __device__ inline size_t m64_words(const DevGraph& g) { return ((size_t)g.m + 31) / 32; }
+__host__ __device__ inline size_t m64_lds_bytes(const DevGraph& g) {
+    return kCtrl + (size_t)2 * g.m * 16 + 7 * 4 * m64_words(g) + 2 * 4 * (kM64Threads / 64);
+}
+
+__device__ __forceinline__ unsigned long long dbits(double x) { return (unsigned long long)__double_as_longlong(x); }
+
+template <int VPT>
+__global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, DecodeArgs a,
+                                                                 const uint16_t* __restrict__ etab,
+                                                                 const double* __restrict__ prior) {
+    static_assert(VPT * 3 <= 32 && VPT <= 32, "degree and decision bits");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    long long* next = reinterpret_cast<long long*>(smem + 56);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m = g.m, n = g.n;
+    const int W = (int)m64_words(g);
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(smem + kCtrl);  // [2][m][2]
+    uint32_t* synw = reinterpret_cast<uint32_t*>(smem + kCtrl + (size_t)2 * m * 16);
+    uint32_t* parw = synw + W;      // [2][W]
+    uint32_t* tiew = parw + 2 * W;  // [2][W]
+    uint32_t* hdw = tiew + 2 * W;   // [2][W]
+    int* flags = reinterpret_cast<int*>(hdw + 2 * W);  // [2][16]
+    const int ncr = tid < m ? (m - tid + kM64Threads - 1) / kM64Threads : 0;  // checks of this thread
+    const int nch = (m + kM64Threads - 1) / kM64Threads;                     // check rounds (uniform)
+    const unsigned long long kBig = dbits(Big<double>::v);
+    constexpr unsigned long long kAbs = 0x7fffffffffffffffull;
+    if (blockIdx.x == 0 && tid == 0) *a.q_count = (int32_t)a.B;
+
+    // per-variable constants: degree, check of each edge (u16 pairs); the priors
+    // are re-read from global memory (L1) where used, to leave the registers to
+    // the messages
+    uint32_t ep[VPT][kMlDC / 2];
+    uint32_t djs = 0;  // 3 bits per owned variable: its degree (real edges come first)
+    auto prior_of = [&](const double* pr, int r) -> double {
+        const int j = r * kM64Threads + tid;
+        return j < n ? pr[j] : 0.0;
+    };
+#pragma unroll
+    for (int r = 0; r < VPT; ++r) {
+        const int j = r * kM64Threads + tid;
+        int dj = 0;
+#pragma unroll
+        for (int h = 0; h < kMlDC / 2; ++h) {
+            uint32_t e0 = 0xffffu, e1 = 0xffffu;
+            if (j < n) {
+                e0 = etab[(size_t)(2 * h) * n + j];
+                e1 = etab[(size_t)(2 * h + 1) * n + j];
+            }
+            dj += (e0 != 0xffffu) + (e1 != 0xffffu);
+            e0 = e0 == 0xffffu ? 0u : e0 / kMlDRS;
+            e1 = e1 == 0xffffu ? 0u : e1 / kMlDRS;
+            ep[r][h] = e0 | (e1 << 16);
+        }
+        djs |= (uint32_t)dj << (3 * r);
+    }
+    auto chk = [&](int r, int k) -> int { return (int)((ep[r][k >> 1] >> (16 * (k & 1))) & 0xffffu); };
+    auto deg = [&](int r) -> int { return (int)((djs >> (3 * r)) & 7u); };
+    // keeps the per-edge addresses from being hoisted out of the loops (as in
+    // bp_ms_lds_kernel): they are re-derived from ep where used
+    auto opaque_edges = [&]() {
+#pragma unroll
+        for (int r = 0; r < VPT; ++r)
+#pragma unroll
+            for (int h = 0; h < kMlDC / 2; ++h) asm volatile("" : "+v"(ep[r][h]));
+        asm volatile("" : "+v"(djs));
+    };
+    // ldpc's (v <= 0) for a v2c message (never -0)
+    auto neg = [](double v) -> uint32_t { return (uint32_t)((dbits(v) - 1ull) >> 63); };
+    // second pass of the messages v on buffer nb: m2 (with multiplicity) from m1
+    auto m2_pass = [&](const double (&v)[VPT][kMlDC], int nb) {
+        opaque_edges();
+#pragma unroll
+        for (int r = 0; r < VPT; ++r) {
+            const int dj = deg(r);
+#pragma unroll
+            for (int k = 0; k < kMlDC; ++k) {
+                if (k < dj) {
+                    const int i = chk(r, k);
+                    unsigned long long* s = st + 2 * ((size_t)nb * m + i);
+                    const unsigned long long m1 = s[0];
+                    const unsigned long long ab = dbits(v[r][k]) & kAbs;
+                    if (ab == m1) {
+                        const uint32_t bit = 1u << (i & 31);
+                        if (atomicOr(&tiew[nb * W + (i >> 5)], bit) & bit) atomicMin(s + 1, m1);
+                    } else {
+                        atomicMin(s + 1, ab);
+                    }
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    for (;;) {
+        if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
+        __syncthreads();
+        const int64_t shot = *next;
+        if (shot >= a.B) break;
+        // ---- S: syndrome words (ballots of 64 consecutive checks), both buffers reset
+        uint32_t sb = 0;  // syndrome bits of the owned checks
+        for (int c = 0; c < nch; ++c) {
+            const int i = c * kM64Threads + tid;
+            const uint32_t s = i < m ? (uint32_t)(a.syn[shot * m + i] & 1) : 0u;
+            sb |= s << c;
+            const unsigned long long bw = __ballot(s != 0u);
+            const int w0 = (c * kM64Threads + wv * 64) >> 5;
+            if (lane < 2 && w0 + lane < W) {
+                const uint32_t word = (uint32_t)(bw >> (32 * lane));
+                synw[w0 + lane] = word;
+                parw[w0 + lane] = word;
+                parw[W + w0 + lane] = word;
+            }
+        }
+        for (int w = tid; w < W; w += kM64Threads) {
+            tiew[w] = tiew[W + w] = 0u;
+            hdw[w] = hdw[W + w] = 0u;
+        }
+        for (int i = tid; i < 2 * m; i += kM64Threads) {
+            st[2 * i] = kBig;
+            st[2 * i + 1] = kBig;
+        }
+        __syncthreads();
+        // ---- iteration 1's check states from v2c = prior (buffer 1)
+        double v[VPT][kMlDC];
+        opaque_edges();
+#pragma unroll
+        for (int r = 0; r < VPT; ++r) {
+            const int dj = deg(r);
+            const double Lr = prior_of(prior, r);
+            const unsigned long long ab = dbits(Lr) & kAbs;
+            const uint32_t ng = neg(Lr);
+#pragma unroll
+            for (int k = 0; k < kMlDC; ++k) {
+                v[r][k] = Lr;
+                if (k < dj) {
+                    const int i = chk(r, k);
+                    atomicMin(st + 2 * ((size_t)m + i), ab);
+                    if (ng) atomicXor(&parw[W + (i >> 5)], 1u << (i & 31));
+                }
+            }
+        }
+        __syncthreads();
+        m2_pass(v, 1);
+        __syncthreads();
+
+        uint32_t xb = 0, bad = 0;  // hard decisions (bit r), failing owned checks (bit c)
+        bool conv = false;
+        int it = 1;
+        for (;; ++it) {
+            const int b = it & 1, nb = b ^ 1;
+            const double alpha = alpha_at<double>(it, a.ms_scaling);
+            // ---- D: c2v from buffer b, sums, hard decision, new v2c -> buffer nb
+            xb = 0;
+            opaque_edges();
+            const double* pr = prior;
+            asm volatile("" : "+s"(pr));  // the prior loads stay in the loop
+#pragma unroll
+            for (int r = 0; r < VPT; ++r) {
+                const int dj = deg(r);
+                const double Lr = prior_of(pr, r);
+                double c[kMlDC];
+#pragma unroll
+                for (int k = 0; k < kMlDC; ++k) {
+                    c[k] = 0.0;
+                    if (k < dj) {
+                        const int i = chk(r, k);
+                        const unsigned long long* s = st + 2 * ((size_t)b * m + i);
+                        const unsigned long long m1 = s[0], m2 = s[1];
+                        const uint32_t pw = parw[b * W + (i >> 5)];
+                        const unsigned long long vb = dbits(v[r][k]);
+                        const double y = __longlong_as_double((long long)((vb & kAbs) == m1 ? m2 : m1)) * alpha;
+                        const uint32_t sg = ((pw >> (i & 31)) ^ (uint32_t)((vb - 1ull) >> 63)) & 1u;
+                        c[k] = __longlong_as_double((long long)(dbits(y) ^ ((unsigned long long)sg << 63)));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // one edge's state in flight (registers)
+                }
+                // ldpc's order: prefix sums from the prior, then each outgoing
+                // message = prefix + (sum of the later edges, accumulated from the end)
+                double pre[kMlDC];
+                double acc = Lr;
+#pragma unroll
+                for (int k = 0; k < kMlDC; ++k) {
+                    pre[k] = acc;
+                    acc = k < dj ? acc + c[k] : acc;
+                }
+                const bool x = acc <= 0.0;
+                xb |= (uint32_t)x << r;
+                double suf = 0.0;
+                bool started = false;
+#pragma unroll
+                for (int k = kMlDC - 1; k >= 0; --k) {
+                    const double o = started ? pre[k] + suf : pre[k];
+                    suf = started ? suf + c[k] : c[k];
+                    started = started || k < dj;
+                    if (k < dj) {
+                        v[r][k] = o;
+                        const int i = chk(r, k);
+                        atomicMin(st + 2 * ((size_t)nb * m + i), dbits(o) & kAbs);
+                        if (neg(o)) atomicXor(&parw[nb * W + (i >> 5)], 1u << (i & 31));
+                        if (x) atomicXor(&hdw[b * W + (i >> 5)], 1u << (i & 31));
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+            // ---- B: syndrome test of iteration it; m2 of the new messages; reset
+            bad = 0;
+            for (int c = 0; c < ncr; ++c) {
+                const int i = c * kM64Threads + tid;
+                bad |= (((hdw[b * W + (i >> 5)] ^ synw[i >> 5]) >> (i & 31)) & 1u) << c;
+            }
+            const unsigned long long wb = __ballot(bad != 0u);
+            if (lane == 0) flags[b * (kM64Threads / 64) + wv] = wb != 0ull;
+            const bool more = it < a.max_iter;
+            if (more) m2_pass(v, nb);
+            for (int i = tid; i < m; i += kM64Threads) {
+                st[2 * ((size_t)b * m + i)] = kBig;
+                st[2 * ((size_t)b * m + i) + 1] = kBig;
+            }
+            for (int w = tid; w < W; w += kM64Threads) {
+                parw[b * W + w] = synw[w];
+                tiew[b * W + w] = 0u;
+                hdw[nb * W + w] = 0u;
+            }
+            __syncthreads();
+            int any_bad = 0;
+#pragma unroll
+            for (int w = 0; w < kM64Threads / 64; ++w) any_bad |= flags[b * (kM64Threads / 64) + w];
+            if (!any_bad) {
+                conv = true;
+                break;
+            }
+            if (!more) break;
+        }
+        // ---- queue the shot: hard decision, residual syndrome, converged bit
+#pragma unroll
+        for (int r = 0; r < VPT; ++r) {
+            const int j = r * kM64Threads + tid;
+            if (j < n) a.q_x[shot * n + j] = (uint8_t)((xb >> r) & 1);
+        }
+        for (int c = 0; c < ncr; ++c) a.q_r[shot * m + c * kM64Threads + tid] = (uint8_t)((bad >> c) & 1);
+        if (tid == 0) {
+            a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
+            if (a.iters) a.iters[shot] = conv ? it : a.max_iter;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launcher
 template <typename K, typename P>
 static int launch_block(K kern, size_t lds, int64_t work, int num_cus, hipStream_t stream, int cap_per_cu,
@@ -1564,12 +1840,20 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
 }
 
 // ---------------------------------------------------------------- LDS-resident launch
-// QD_OPT_LDS_KERNEL = 0 disables bp_ms_lds_kernel, 1 forces it on any graph it can
-// hold (also those whose messages fit the small-graph LDS budget); by default
-// it takes the min-sum fp32 graphs whose messages would go to HBM.
+// QD_OPT_LDS_KERNEL = 0 disables bp_ms_lds_kernel / bp_ms_lds64_kernel, 1 forces
+// them on any graph they can hold (also those whose messages fit the small-graph
+// LDS budget); by default they take the min-sum graphs whose messages would go
+// to HBM (f32: edge slots <= 160 KB; f64: n <= 10240 and the check states <= 160 KB).
 bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a) {
-    if (method != 1 || precision != 1 || !g.ml_etab) return false;
+    if (method != 1 || !g.ml_etab) return false;
     if (!a.syn || a.syn_flags || a.llr_out || !a.wave_ctr) return false;
+    if (precision == 0) {  // bp_ms_lds64_kernel (automatic: graphs whose messages would go to HBM)
+        if (g.n > 10 * kM64Threads || g.m <= 0 || g.m > 32 * kM64Threads || a.max_iter < 1) return false;
+        if (m64_lds_bytes(g) > 160 * 1024 || block_placement(g, 8) == 0) return false;
+        if (g.opt_lds_kernel == 0) return false;
+        return g.opt_lds_kernel == 1 || block_placement(g, 8) != 3;
+    }
+    if (precision != 1) return false;
     if (g.n > 16 * kMlThreads || g.m <= 0 || ml_lds_bytes(g) > 160 * 1024) return false;
     if (block_placement(g, 4) == 0) return false;  // the SSF/finalize state would not fit LDS
     if (g.opt_lds_kernel == 0) return false;
@@ -1604,8 +1888,39 @@ static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus,
     return rc;
 }
 
-static int launch_lds(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+template <int VPT>
+static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+    const size_t lds = m64_lds_bytes(g);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bp_ms_lds64_kernel<VPT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_ms_lds64_kernel<VPT>, kM64Threads, lds);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    const long long grid = std::min<long long>((long long)num_cus * per_cu, a.B);
+    e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);  // shot counter
+    if (e != hipSuccess) return (int)e;
+    record_ev(a, 0, stream);
+    QDEC_NOTE_BP("qdec::bp_ms_lds64_kernel", VPT);
+    hipLaunchKernelGGL((bp_ms_lds64_kernel<VPT>), dim3((unsigned)grid), dim3(kM64Threads), lds, stream, g, a,
+                       g.ml_etab, reinterpret_cast<const double*>(g.prior[1][0]));
+    const hipError_t le = hipGetLastError();
+    record_ev(a, 1, stream);
+    if (le != hipSuccess) return (int)le;
+    const int rc = launch_ssf_fin(g, a, num_cus, stream);
+    record_ev(a, 2, stream);
+    return rc;
+}
+
+static int launch_lds(const DevGraph& g, int precision, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+    if (precision == 0) {
+        const int vpt = (g.n + kM64Threads - 1) / kM64Threads;
+        if (vpt <= 4) return launch_lds64_typed<4>(g, a, num_cus, stream);
+        if (vpt <= 8) return launch_lds64_typed<8>(g, a, num_cus, stream);
+        return launch_lds64_typed<10>(g, a, num_cus, stream);
+    }
     const int vpt = (g.n + kMlThreads - 1) / kMlThreads;
     if (vpt <= 4) return launch_lds_typed<4>(g, a, num_cus, stream);
     if (vpt <= 8) return launch_lds_typed<8>(g, a, num_cus, stream);
@@ -1773,7 +2088,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
         return method == 1 ? launch_group_shape<double, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_group_shape<double, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
     }
-    if (lds) return launch_lds(g, a, num_cus, stream);
+    if (lds) return launch_lds(g, precision, a, num_cus, stream);
     if (precision == 1)
         return method == 1 ? launch_block_typed<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_block_typed<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);

@@ -236,7 +236,9 @@ int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int3
  *                        kernel, local syndromes re-gathered every step),
  *                        QD_SSF_SCAN_NOSPLIT (scanning, one lane per generator).
  *   QD_OPT_LDS_KERNEL    -1 (default) automatic, 0 never, 1 forced: the
- *                        LDS-resident f32 min-sum workgroup kernel.
+ *                        LDS-resident min-sum workgroup kernels (f32: every
+ *                        message in LDS; f64: v2c in registers, check states
+ *                        by LDS atomics).
  *   QD_OPT_GROUP_KERNEL  -1 (default) automatic, 0 never, 1 forced: the slot-group
  *                        HBM-streaming kernel.
  *   QD_OPT_SSF_INC       1 (default): incremental workgroup SSF; 0: re-scanning.

@@ -3,7 +3,8 @@ package's own code sources (exp_ldpc_amd/hgp.py, lifted.py):
 
 * C3  [[144,12,12]] bivariate-bicycle lift -> wave kernels, BP + SSF
 * C4  biregular_hgp(80,3,4,seed=2025), n = 10^4 (reference-generated fixture)
-      -> workgroup kernels with HBM message scratch, BP + SSF
+      -> the LDS-resident kernels (f32 and f64) and the HBM-message workgroup /
+      slot-group kernels, BP + SSF
 * C5  as BASELINE names it: the PSL(2,16) Cayley-graph lifted-product code
       lifted_product_code_pgl2(1, 4, 2, double_cover=False, seed=1), n = 53,040,
       k = 4080 (fixture tests/golden/lp_pgl2_1_4_2_s1_*): BP + SSF + logical check
@@ -99,10 +100,14 @@ def test_hgp10k_group_kernel_forced_parity(gpu_available, oracle_lib, hgp10k, mo
     assert got["ssf_steps"].sum() > 0
 
 
+@pytest.mark.parametrize("kernel", ["auto", "group"])
 @pytest.mark.parametrize("p", [0.01, 0.03])
-def test_hgp10k_f64_bp_ssf_fail_parity(gpu_available, oracle_lib, hgp10k, p):
-    """C4 at ldpc's precision: BP min-sum f64 max_iter 50 (the slot-group kernel,
-    messages in HBM) + SSF + logical check, 256 sampled shots, bit-exact."""
+def test_hgp10k_f64_bp_ssf_fail_parity(gpu_available, oracle_lib, hgp10k, p, kernel, monkeypatch):
+    """C4 at ldpc's precision: BP min-sum f64 max_iter 50 (auto: the LDS-resident
+    bp_ms_lds64_kernel; group: the slot-group kernel, messages in HBM, with
+    QD_OPT_LDS_KERNEL = 0) + SSF + logical check, 256 sampled shots, bit-exact."""
+    if kernel == "group":
+        monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 0)
     hx, hz, lz = hgp10k
     syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=14, shot0=0, B=256)
     got = _decode_both(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=50, precision="f64",
@@ -251,6 +256,83 @@ def test_lds_kernel_zero_and_negative_priors(gpu_available, oracle_lib, monkeypa
     probs = rng.choice([0.5, 0.5, 0.6, 0.02, 0.05, 0.01], n)
     for scaling in (0.0, 0.625):
         _decode_both(oracle_lib, H, probs, syn, max_iter=20, ms_scaling=scaling)
+
+
+def _decode_lds64(oracle_lib, H, prior, syn, **kw):
+    """_decode_both at f64 with bp_ms_lds64_kernel forced; asserts it ran."""
+    from exp_ldpc_amd.decoder import Decoder
+    keys = kw.pop("keys", ("x", "iters", "status"))
+    rd, gens, lz = kw.pop("rd", None), kw.pop("gens", None), kw.pop("lz", None)
+    max_iter = kw.pop("max_iter", 50)
+    dec = Decoder(H, prior, method="ms", precision="f64", max_iter=max_iter, flip_sets=gens, logicals=lz, **kw)
+    got = dec.decode(syn, readout=rd, want=keys)
+    assert "bp_ms_lds64_kernel" in dec.last_kernels()[0]
+    ref = oracle_lib.decode(H, prior, syn, method="ms", precision="f64", max_iter=max_iter, ssf=gens is not None,
+                            gens=gens, lz=lz, readout=rd, want_llr=False, ssf_impl="fast", **kw)
+    for k in keys:
+        assert np.array_equal(got[k], ref[k]), k
+    return got
+
+
+@pytest.mark.parametrize("p", [0.005, 0.03, 0.06])
+def test_hgp10k_lds64_kernel_parity(gpu_available, oracle_lib, hgp10k, p, monkeypatch):
+    """C4 at ldpc's precision on the LDS-resident f64 kernel (bp_ms_lds64_kernel:
+    v2c messages in registers, check states by LDS atomics; QD_OPT_LDS_KERNEL = 1):
+    x / corrections / iterations / status / SSF steps / failure flags bit-exact,
+    low to high p (the last runs most shots to max_iter)."""
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
+    hx, hz, lz = hgp10k
+    syn, rd = oracle_lib.sample_storage(hz, 0, p, p, seed=SEED, stream=15, shot0=0, B=256)
+    got = _decode_lds64(oracle_lib, hz, 2 * p / 3, syn, rd=rd, gens=hx, lz=lz, max_iter=50, keys=KEYS_SSF)
+    if p >= 0.03:
+        assert (got["status"] & 1).mean() < 0.9 and got["ssf_steps"].sum() > 0
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_lds64_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatch):
+    """bp_ms_lds64_kernel on ragged graphs: check degrees 0..8 (empty and
+    single-edge rows: m2 stays Big), variable degrees 0..4, per-column priors,
+    ms_scaling both ways, max_iter 1 and 30; x / iterations / status."""
+    from exp_ldpc_amd.codes import make_check_matrix
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
+    rng = np.random.default_rng(seed)
+    m, n = int(rng.integers(600, 1500)), int(rng.integers(700, 3000))
+    rows, colcount = [], np.zeros(n, int)
+    for i in range(m):
+        d = int(rng.integers(0, 9))
+        cand = [j for j in rng.permutation(n) if colcount[j] < 4][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    H = make_check_matrix(rows, n)
+    e = (rng.random((300, n)) < 0.02).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.uniform(0.005, 0.1, n)
+    for scaling in (0.0, 0.625):
+        _decode_lds64(oracle_lib, H, probs, syn, max_iter=30, ms_scaling=scaling)
+    _decode_lds64(oracle_lib, H, probs, syn, max_iter=1)
+
+
+def test_lds64_kernel_zero_and_negative_priors(gpu_available, oracle_lib, monkeypatch):
+    """bp_ms_lds64_kernel on exactly-zero messages (p = 0.5 columns: +0 priors,
+    ties at m1 = 0, -0 c2v) and negative priors (p > 0.5)."""
+    from exp_ldpc_amd.codes import make_check_matrix
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
+    rng = np.random.default_rng(5)
+    m, n = 900, 1600
+    rows, colcount = [], np.zeros(n, int)
+    for i in range(m):
+        d = int(rng.integers(2, 9))
+        cand = [j for j in rng.permutation(n) if colcount[j] < 4][:d]
+        for j in cand:
+            colcount[j] += 1
+        rows.append(sorted(cand))
+    H = make_check_matrix(rows, n)
+    e = (rng.random((300, n)) < 0.03).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.choice([0.5, 0.5, 0.6, 0.02, 0.05, 0.01], n)
+    for scaling in (0.0, 0.625):
+        _decode_lds64(oracle_lib, H, probs, syn, max_iter=20, ms_scaling=scaling)
 
 
 @pytest.mark.parametrize("scoring", ["auto", "scan"])

@@ -1,4 +1,7 @@
-"""Throughput benchmark: decoded syndrome shots/s + logical error rate on the
+"""Diagnostic copy of bench.py (--no-ssf-exp: decode without SSF, to price SSF in
+the overlapped step).
+
+Throughput benchmark: decoded syndrome shots/s + logical error rate on the
 (3,4)-HGP n=225 code (BASELINE.json configs[1] = SURVEY §8(d) C2).
 
 One step = one pass of the hot path over one batch per sweep point: for each
@@ -72,9 +75,10 @@ import time
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 
+NOSSF = None  # set by --no-ssf-exp
 from exp_ldpc_amd.sharding import barrier, gather_rows, max_time, reduce_counts  # noqa: E402  (pure Python, no GPU)
 
 METRIC = "decoded syndrome shots/sec + logical error rate, (3,4)-HGP n=225 @ 1/2/4/8 GPUs"
@@ -327,10 +331,8 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
     finishes, and at low p (2-6 iterations per shot) that tail weighs against
     2^17 / 256 groups = 512 shots per group; the config itself decodes 1e7
     shots.
-    f64 runs bp_ms_lds64_kernel (v2c messages in registers, check states built
-    by LDS atomics: LDS roofline, 44 B per edge + 16 B per check per
-    shot-iteration; the slot-group kernel's HBM model, 32 B per edge per
-    shot-iteration + I/O, applies when a handle forces it); f32 runs the LDS-resident kernel
+    f64 runs the slot-group kernel (messages stream through HBM: HBM roofline,
+    32 B per edge per shot-iteration + I/O); f32 runs the LDS-resident kernel
     (every message on chip: LDS roofline, per shot-iteration 8 B per edge -- the
     variable pass reads the edge's c2v slot and writes its v2c back -- and 64 B
     per check -- the check pass reads its 32-B row of v2c and writes it back as
@@ -376,14 +378,7 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
             kern = dec.last_kernels()
             it_sum = int(iters[1].to(torch.int64).sum().item())
             io = shots * (m + n + 1 + 1 + 4)
-            if "lds64" in kern[0]:
-                algo = (44 * E + 16 * m) * it_sum
-                roof = {"bound": "lds", "peak": LDS_PEAK_GBS,
-                        "bytes_model": "LDS: 44 B per edge + 16 B per check per shot-iteration (variable pass: 16-B "
-                                       "(m1, m2) state + parity word read, ds_min_u64 on the next m1; second pass: m1 "
-                                       "read + ds_min_u64 on m2; check state reset), the data-dependent sign / "
-                                       "decision xors not counted"}
-            elif "group" in kern[0]:
+            if "group" in kern[0]:
                 algo = 32 * E * it_sum + io
                 roof = {"bound": "hbm", "peak": HBM_PEAK_GBS,
                         "bytes_model": "32 B per edge per shot-iteration (f64 messages through HBM: v2c read + c2v "
@@ -597,7 +592,7 @@ class Run:
         for j, pi in enumerate(order):
             st = streams[j % len(streams)]
             decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
-                                   status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi],
+                                   status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi], ssf=NOSSF,
                                    stream=st.cuda_stream)
         if join:
             for st in streams[1:]:
@@ -657,6 +652,7 @@ def main():
     ap.add_argument("--wave-occupancy", type=int, default=-1,
                     help="waves per CU of the wave BP kernels in the overlapped phases (qd_graph_set_wave_occupancy); "
                          "-1 = 12 for f64 when the points share the chip over several streams, else the default")
+    ap.add_argument("--no-ssf-exp", action="store_true")
     ap.add_argument("--step-join", default="end", choices=["step", "end"],
                     help="streams schedule: join every point's stream at the end of each step (step) or only at the "
                          "end of the timed region (end: each point's steps run back to back on its stream)")
@@ -671,6 +667,8 @@ def main():
                     help="skip the reference-default bposd line (reference_default_line; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    global NOSSF
+    NOSSF = False if args.no_ssf_exp else None
     args.iso_steps = max(1, min(args.iso_steps, args.steps))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
