@@ -1483,6 +1483,11 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     uint32_t* tiew = parw + 2 * W;  // [2][W]
     uint32_t* hdw = tiew + 2 * W;   // [2][W]
     int* flags = reinterpret_cast<int*>(hdw + 2 * W);  // [2][16]
+    // variable slot of this thread: tid * 67 mod 1024, so the 64 lanes of a wave own
+    // columns 67 apart instead of 64 neighbours (neighbouring columns of a
+    // hypergraph product share checks, and lanes of one wave hitting one check's
+    // state serialise its atomics)
+    const int tq = (tid * 67) & (kM64Threads - 1);
     const int ncr = tid < m ? (m - tid + kM64Threads - 1) / kM64Threads : 0;  // checks of this thread
     const int nch = (m + kM64Threads - 1) / kM64Threads;                     // check rounds (uniform)
     const unsigned long long kBig = dbits(Big<double>::v);
@@ -1495,12 +1500,12 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     uint32_t ep[VPT][kMlDC / 2];
     uint32_t djs = 0;  // 3 bits per owned variable: its degree (real edges come first)
     auto prior_of = [&](const double* pr, int r) -> double {
-        const int j = r * kM64Threads + tid;
+        const int j = r * kM64Threads + tq;
         return j < n ? pr[j] : 0.0;
     };
 #pragma unroll
     for (int r = 0; r < VPT; ++r) {
-        const int j = r * kM64Threads + tid;
+        const int j = r * kM64Threads + tq;
         int dj = 0;
 #pragma unroll
         for (int h = 0; h < kMlDC / 2; ++h) {
@@ -1515,6 +1520,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             ep[r][h] = e0 | (e1 << 16);
         }
         djs |= (uint32_t)dj << (3 * r);
+        __builtin_amdgcn_sched_barrier(0);  // one variable's loads at a time (registers)
     }
     auto chk = [&](int r, int k) -> int { return (int)((ep[r][k >> 1] >> (16 * (k & 1))) & 0xffffu); };
     auto deg = [&](int r) -> int { return (int)((djs >> (3 * r)) & 7u); };
@@ -1615,8 +1621,9 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             // ---- D: c2v from buffer b, sums, hard decision, new v2c -> buffer nb
             xb = 0;
             opaque_edges();
-            const double* pr = prior;
-            asm volatile("" : "+s"(pr));  // the prior loads stay in the loop
+            int pz = 0;
+            asm volatile("" : "+s"(pz));  // the prior loads stay in the loop (global, not flat)
+            const double* pr = prior + pz;
 #pragma unroll
             for (int r = 0; r < VPT; ++r) {
                 const int dj = deg(r);
@@ -1698,7 +1705,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
         // ---- queue the shot: hard decision, residual syndrome, converged bit
 #pragma unroll
         for (int r = 0; r < VPT; ++r) {
-            const int j = r * kM64Threads + tid;
+            const int j = r * kM64Threads + tq;
             if (j < n) a.q_x[shot * n + j] = (uint8_t)((xb >> r) & 1);
         }
         for (int c = 0; c < ncr; ++c) a.q_r[shot * m + c * kM64Threads + tid] = (uint8_t)((bad >> c) & 1);
