@@ -1440,8 +1440,8 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
 // iteration in registers, and the check side is reduced to its min-sum state,
 // built by LDS atomics on the IEEE bit patterns (|v| >= +0 orders like an
 // unsigned integer, so ds_min_u64 is the exact minimum):
-//   st[b][i]  (m1, m2) as u64 bits: minimum and second minimum of |v| over the
-//             row, with multiplicity (a repeated minimum gives m2 = m1)
+//   m1[b][i], m2[b][i]  u64 bits (two arrays): minimum and second minimum of
+//             |v| over the row, with multiplicity (a repeated minimum gives m2 = m1)
 //   parw[b]   per check: syndrome ^ parity of (v <= 0) over the row
 //   tiew[b]   per check: "an edge with |v| == m1 was seen" (the second such edge
 //             sets m2 = m1)
@@ -1477,7 +1477,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int m = g.m, n = g.n;
     const int W = (int)m64_words(g);
-    unsigned long long* st = reinterpret_cast<unsigned long long*>(smem + kCtrl);  // [2][m][2]
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(smem + kCtrl);  // m1 [2][m], then m2 [2][m]
     uint32_t* synw = reinterpret_cast<uint32_t*>(smem + kCtrl + (size_t)2 * m * 16);
     uint32_t* parw = synw + W;      // [2][W]
     uint32_t* tiew = parw + 2 * W;  // [2][W]
@@ -1545,14 +1545,14 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             for (int k = 0; k < kMlDC; ++k) {
                 if (k < dj) {
                     const int i = chk(r, k);
-                    unsigned long long* s = st + 2 * ((size_t)nb * m + i);
+                    unsigned long long* s = st + (size_t)nb * m + i;  // m1; m2 at s + 2m
                     const unsigned long long m1 = s[0];
                     const unsigned long long ab = dbits(v[r][k]) & kAbs;
                     if (ab == m1) {
                         const uint32_t bit = 1u << (i & 31);
-                        if (atomicOr(&tiew[nb * W + (i >> 5)], bit) & bit) atomicMin(s + 1, m1);
+                        if (atomicOr(&tiew[nb * W + (i >> 5)], bit) & bit) atomicMin(s + 2 * (size_t)m, m1);
                     } else {
-                        atomicMin(s + 1, ab);
+                        atomicMin(s + 2 * (size_t)m, ab);
                     }
                 }
             }
@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 v[r][k] = Lr;
                 if (k < dj) {
                     const int i = chk(r, k);
-                    atomicMin(st + 2 * ((size_t)m + i), ab);
+                    atomicMin(st + (size_t)m + i, ab);
                     if (ng) atomicXor(&parw[W + (i >> 5)], 1u << (i & 31));
                 }
             }
@@ -1634,8 +1634,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                     c[k] = 0.0;
                     if (k < dj) {
                         const int i = chk(r, k);
-                        const unsigned long long* s = st + 2 * ((size_t)b * m + i);
-                        const unsigned long long m1 = s[0], m2 = s[1];
+                        const unsigned long long* s = st + (size_t)b * m + i;
+                        const unsigned long long m1 = s[0], m2 = s[2 * (size_t)m];
                         const uint32_t pw = parw[b * W + (i >> 5)];
                         const unsigned long long vb = dbits(v[r][k]);
                         const double y = __longlong_as_double((long long)((vb & kAbs) == m1 ? m2 : m1)) * alpha;
@@ -1665,7 +1665,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                     if (k < dj) {
                         v[r][k] = o;
                         const int i = chk(r, k);
-                        atomicMin(st + 2 * ((size_t)nb * m + i), dbits(o) & kAbs);
+                        atomicMin(st + (size_t)nb * m + i, dbits(o) & kAbs);
                         if (neg(o)) atomicXor(&parw[nb * W + (i >> 5)], 1u << (i & 31));
                         if (x) atomicXor(&hdw[b * W + (i >> 5)], 1u << (i & 31));
                     }
@@ -1684,8 +1684,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             const bool more = it < a.max_iter;
             if (more) m2_pass(v, nb);
             for (int i = tid; i < m; i += kM64Threads) {
-                st[2 * ((size_t)b * m + i)] = kBig;
-                st[2 * ((size_t)b * m + i) + 1] = kBig;
+                st[(size_t)b * m + i] = kBig;
+                st[(size_t)(2 + b) * m + i] = kBig;
             }
             for (int w = tid; w < W; w += kM64Threads) {
                 parw[b * W + w] = synw[w];

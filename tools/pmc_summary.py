@@ -110,7 +110,7 @@ def main():
         json.dump(res, fh, indent=1)
     for k, v in sorted(kernels.items()):
         if family(k) in ("bp_ms_wave_kernel", "bp_wave_kernel", "bp_block_kernel", "ssf_wave_kernel",
-                         "ssf_block_kernel", "bp_group_kernel", "bp_ms_lds_kernel", "ssf_inc_block_kernel"):
+                         "ssf_block_kernel", "bp_group_kernel", "bp_ms_lds_kernel", "bp_ms_lds64_kernel", "ssf_inc_block_kernel"):
             print(k[:100], v["dispatches"], {a: (round(b, 4) if isinstance(b, float) else None)
                                                for a, b in v["derived"].items() if a != "formulas"})
 
