@@ -244,15 +244,18 @@ def cpu_baseline(code, ps, args):
     return res
 
 
-def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
+def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.002, 0.005)):
     """HBM roofline of the genuinely HBM-bound path: BASELINE config 5 (PSL(2,16)
     Cayley-graph LP code, n = 53,040) at R = 1 spacetime syndromes (H_st
     48,960 x 130,560, E = 236,640), BP min-sum f64 max_iter 50 + fold + logical
-    check on the slot-group kernel, whose messages stream through HBM.  One
-    warmup launch, one timed launch (HIP events around the BP kernel on its
-    launch stream).  Algorithmic bytes = 32 B per edge per shot-iteration (f64
-    v2c read + c2v write in the check pass, c2v read + v2c write in the column
-    pass) + the per-shot I/O (syndrome, readout, outputs)."""
+    check on the slot-group kernel, whose messages stream through HBM.  Per p:
+    one warmup launch, one timed launch (HIP events around the BP kernel on its
+    launch stream).  The first p (0.002) is a point where BP converges and the
+    code decodes (the line's headline); the last (0.005) is the worst case where
+    every shot runs all 50 iterations (LER ~1), kept as the bandwidth figure.
+    Algorithmic bytes = 32 B per edge per shot-iteration (f64 v2c read + c2v
+    write in the check pass, c2v read + v2c write in the column pass) + the
+    per-shot I/O (syndrome, readout, outputs)."""
     import scipy.sparse as sp
     import torch
     from exp_ldpc_amd.decoder import Decoder
@@ -267,50 +270,123 @@ def large_code_roofline(dev, shots: int = 1 << 16, p: float = 0.005):
     H = sp.csr_matrix(SpacetimeCode(hz, 1).spacetime_check_matrix)
     m, n = H.shape
     nd = hz.shape[1]
-    sampler = Decoder(hz, 2 * p / 3, method="ms", precision="f64", max_iter=50, device=dev.index)
-    dec = Decoder(H, 2 * p / 3, method="ms", precision="f64", max_iter=50, logicals=lz, n_data=nd, fold_blocks=2,
+    E = int(H.nnz)
+    sampler = Decoder(hz, 2 * ps[0] / 3, method="ms", precision="f64", max_iter=50, device=dev.index)
+    dec = Decoder(H, 2 * ps[0] / 3, method="ms", precision="f64", max_iter=50, logicals=lz, n_data=nd, fold_blocks=2,
                   device=dev.index)
     syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
     rd = torch.empty((2, shots, nd), dtype=torch.uint8, device=dev)
-    for b in range(2):
-        sampler.sample_storage_device(1, p, p, SEED, 100, b * shots, shots, syn[b], rd[b])
     iters = torch.empty((2, shots), dtype=torch.int32, device=dev)
     status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
     fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
-    dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
-    torch.cuda.synchronize(dev)
-    dec.set_timing(1)
-    t0 = time.perf_counter()
-    dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1])
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    bp_ms, _ = dec.read_timing()
-    it_sum = int(iters[1].to(torch.int64).sum().item())
-    E = int(H.nnz)
-    io = shots * (m + nd + 1 + 1 + 4)
-    algo = 32 * E * it_sum + io
-    achieved = algo / (float(bp_ms[0]) * 1e-3) / 1e9
+    kernel = "qdec::bp_group_kernel<double, 1, 8, 4>"
+    pmc = pmc_ceilings(kernel)
+    lines = []
+    for p in ps:
+        dec.set_priors(np.full(n, 2 * p / 3))
+        for b in range(2):
+            sampler.sample_storage_device(1, p, p, SEED, 100, b * shots, shots, syn[b], rd[b])
+        dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
+        torch.cuda.synchronize(dev)
+        dec.set_timing(1)
+        t0 = time.perf_counter()
+        dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1])
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        bp_ms, _ = dec.read_timing()
+        kernel = dec.last_kernels()[0] or kernel
+        it_sum = int(iters[1].to(torch.int64).sum().item())
+        io = shots * (m + nd + 1 + 1 + 4)
+        algo = 32 * E * it_sum + io
+        achieved = algo / (float(bp_ms[0]) * 1e-3) / 1e9
+        row = {"p": p, "shots_per_s": shots / wall, "bp_kernel_ms": float(bp_ms[0]), "mean_bp_iters": it_sum / shots,
+               "bp_converged_frac": float((status[1] & 1).to(torch.float64).mean().item()),
+               "ler": float(fail[1].to(torch.float64).mean().item()),
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": algo}}
+        if pmc is not None and pmc[2].get("config_p") in (None, p):
+            src, name, k = pmc
+            row["roofline"]["traffic"] = k["derived"].get("hbm_bytes_per_dispatch")
+            row["roofline"]["traffic_source"] = src
+        lines.append(row)
     res = {"config": "C5 as named: PSL(2,16) Cayley-graph LP (lifted_product_code_pgl2(1,4,2,double_cover=False,"
                      "seed=1)), n=53040 k=4080, R=1 spacetime 48960x130560 E=236640, BP min-sum f64 max_iter 50, "
-                     f"fold + logical check, p={p}, {shots} device-sampled shots per launch",
-           "kernel": "qdec::bp_group_kernel<double, 1, 8, 4> (slot groups, messages in HBM)",
-           "shots_per_s": shots / wall, "bp_kernel_ms": float(bp_ms[0]), "mean_bp_iters": it_sum / shots,
-           "ler": float(fail[1].to(torch.float64).mean().item()),
-           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                        "algorithmic_bytes_per_launch": algo,
-                        "bytes_model": "32 B per edge per shot-iteration (f64 messages: v2c read + c2v write, c2v "
-                                       "read + v2c write) + per-shot I/O"}}
-    pmc = pmc_ceilings("qdec::bp_group_kernel<double, 1, 8, 4>")
-    if pmc is not None:  # committed PMC passes of the same launch shape (tools/gpu/r03f.sh)
-        src, name, k = pmc
-        dv = k["derived"]
-        res["roofline"]["traffic"] = dv.get("hbm_bytes_per_dispatch")
-        res["roofline"]["traffic_source"] = {"source": src, "kernel": name, "duration_ms": dv.get("duration_ms"),
-                                             "note": "2*FETCH_SIZE + WRITE_SIZE per dispatch, same config/shots"}
+                     f"fold + logical check, {shots} device-sampled shots per launch",
+           "kernel": kernel,
+           "bytes_model": "32 B per edge per shot-iteration (f64 messages: v2c read + c2v write, c2v read + v2c "
+                          "write) + per-shot I/O",
+           "lines": lines}
     del syn, rd, dec, sampler
     torch.cuda.empty_cache()
     return res
+
+
+def c3_line(dev, shots: int = 1 << 22, ps=(0.001, 0.003, 0.01), precision: str = "f64"):
+    """BASELINE config 3 on one GPU: the [[144,12,12]] bivariate-bicycle lift
+    (quasi-cyclic lifted product over Z_12 x Z_6, built by
+    exp_ldpc_amd.lifted.bivariate_bicycle_code; reference construction
+    matrix_lifted_product_code.py:105-212), R = 0 (Hz 72 x 144, E = 432), BP
+    min-sum f64 max_iter 50 + SSF (Hx flip sets) + logical check.  Per p: one
+    warmup launch and one timed launch of `shots` device-sampled shots (2^22:
+    0.42 of the config's 1e7 per point), HIP events around the triage, BP and
+    SSF kernels.  The BP kernel is the headline's wave kernel family, so the
+    roofline is the headline's LDS model (32 B per edge + 16 B per check per
+    shot-iteration of the shots the BP kernel decoded)."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder
+    from exp_ldpc_amd.lifted import bivariate_bicycle_code
+    code = bivariate_bicycle_code(12, 6, [(3, 0), (0, 1), (0, 2)], [(0, 3), (1, 0), (2, 0)], compute_logicals=True)
+    hz, hx, lz = code.checks.z, code.checks.x, code.logicals.z
+    m, n = hz.shape
+    E = int(hz.nnz)
+    lds_per_it = 32 * E + 16 * m
+    syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
+    rd = torch.empty((2, shots, n), dtype=torch.uint8, device=dev)
+    iters = torch.empty((2, shots), dtype=torch.int32, device=dev)
+    status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+    fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+    steps = torch.empty((2, shots), dtype=torch.int32, device=dev)
+    lines = []
+    for p in ps:
+        dec = Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0, flip_sets=hx,
+                      logicals=lz, device=dev.index)
+        for b in range(2):
+            dec.sample_storage_device(0, p, p, SEED, 400, b * shots, shots, syn[b], rd[b])
+        dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0],
+                          ssf_steps=steps[0])
+        torch.cuda.synchronize(dev)
+        dec.set_timing(1)
+        t0 = time.perf_counter()
+        dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1],
+                          ssf_steps=steps[1])
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        pre_ms, bp_ms, ssf_ms, listed = dec.read_timing_detail()
+        kern = dec.last_kernels()
+        it_sum = int(iters[1].to(torch.int64).sum().item())
+        it_bp = it_sum - (shots - int(listed[0])) if listed[0] >= 0 else it_sum
+        ach = lds_per_it * it_bp / (float(bp_ms[0]) * 1e-3) / 1e9
+        fails = int(fail[1].to(torch.int64).sum().item())
+        lines.append({"p": p, "shots": shots, "shots_per_s": shots / wall, "failures": fails, "ler": fails / shots,
+                      "wilson95": list(wilson(fails, shots)),
+                      "bp_converged_frac": float((status[1] & 1).to(torch.float64).mean().item()),
+                      "mean_bp_iters": it_sum / shots, "triage_ms": float(pre_ms[0]), "bp_kernel_ms": float(bp_ms[0]),
+                      "ssf_kernel_ms": float(ssf_ms[0]), "listed_frac": float(listed[0]) / shots,
+                      "bp_kernel": kern[0], "ssf_kernel": kern[1], "pre_kernel": kern[2],
+                      "roofline": {"bound": "lds", "achieved": ach, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                                   "frac": ach / LDS_PEAK_GBS, "traffic": None,
+                                   "algorithmic_bytes_per_launch": lds_per_it * it_bp},
+                      "hbm_frac_bp_stage": shots * (m + n + 6) / ((float(pre_ms[0]) + float(bp_ms[0])) * 1e-3) / 1e9
+                      / HBM_PEAK_GBS})
+        del dec
+    del syn, rd
+    torch.cuda.empty_cache()
+    return {"config": f"C3: [[144,12,12]] bivariate-bicycle lift (BB 12x6, a=x^3+y+y^2, b=y^3+x+x^2), R=0 "
+                      f"(Hz {m}x{n}, E={E}), BP min-sum {precision} max_iter 50 + SSF + logical check, {shots} "
+                      "device-sampled shots per timed launch",
+            "m": m, "n": n, "E": E, "bytes_model": f"LDS: 32 B per edge + 16 B per check per shot-iteration "
+                                                   f"({lds_per_it} B) of the BP kernel's shots",
+            "lines": lines}
 
 
 def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64", "f32")):
@@ -537,6 +613,7 @@ class Run:
         self.fail = torch.empty((self.nsteps, P, self.B), **u8)
         self.ssf_steps = torch.empty((self.nsteps, P, self.B), dtype=torch.int32, device=dev)
         self.ssf_stream = None
+        self.ssf = False if args.no_ssf_exp else None  # None: the handle's flip sets decide (SSF on)
         if fake:
             self.streams = [None]
         else:
@@ -575,7 +652,7 @@ class Run:
             for pi in range(len(self.ps)):
                 decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                        status=self.status[s, pi], fail=self.fail[s, pi],
-                                       ssf_steps=self.ssf_steps[s, pi], stream=streams[0].cuda_stream)
+                                       ssf_steps=self.ssf_steps[s, pi], ssf=self.ssf, stream=streams[0].cuda_stream)
             ev = torch.cuda.Event()
             ev.record(self.ssf_stream)
             streams[0].wait_event(ev)
@@ -584,7 +661,7 @@ class Run:
             for pi in range(len(self.ps)):
                 decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                        status=self.status[s, pi], fail=self.fail[s, pi],
-                                       ssf_steps=self.ssf_steps[s, pi],
+                                       ssf_steps=self.ssf_steps[s, pi], ssf=self.ssf,
                                        **({} if self.fake else {"stream": streams[0].cuda_stream}))
             return
         join = self.args.step_join == "step"
@@ -598,7 +675,7 @@ class Run:
             st = streams[j % len(streams)]
             decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                    status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi],
-                                   stream=st.cuda_stream)
+                                   ssf=self.ssf, stream=st.cuda_stream)
         if join:
             for st in streams[1:]:
                 e2 = torch.cuda.Event()
@@ -635,6 +712,109 @@ class Run:
         return fails, conv, itp, ssp
 
 
+LINE_MAX_BYTES = 8000  # the driver's parser; round 5's 20 KB line was not read (tests/test_bench_launcher.py)
+
+
+def _r(x, nd: int = 4):
+    """Round a float to `nd` significant digits for the compact line."""
+    if x is None or isinstance(x, (bool, int, str)):
+        return x
+    return float(f"{float(x):.{nd}g}")
+
+
+def compact_line(full: dict, detail: str) -> dict:
+    """The one stdout line rank 0 prints: the contract's fields, the roofline and
+    CPU-baseline blocks, the LER curve as one row per p (the reference's own
+    record, misc/p_sweep.py:32-33: p, failures, samples), and one number + its
+    roofline fraction per extra config.  Everything else (per-point roofline,
+    every config line, sub-records) stays in the side file `detail`."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: full[k] for k in keep if k in full}
+    line["value"] = _r(line["value"], 6)
+    line["ms_per_step"] = _r(line["ms_per_step"], 6)
+    cfg = full["config"]
+    line["config"] = {k: cfg[k] for k in ("workload", "shots_per_point_per_step_per_gpu", "global_batch", "parallelism")}
+    line["ranks_seen"] = full["ranks_seen"]
+    line["ranks"] = [{"rank": x["rank"], "device": x["device"], "timed_s": _r(x["timed_s"], 6), "shots": x["shots"]}
+                     for x in full["ranks"]][:16]
+    rf = full["roofline"]
+    roof = {k: _r(rf.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "avg_launch_ms",
+                                       "launches", "algorithmic_bytes_per_launch")}
+    roof["kernel"] = rf.get("kernel")
+    roof["bytes_model"] = "LDS: 32 B/edge + 16 B/check per shot-iteration of the BP kernel's shots"
+    if "lds_busy_pmc" in rf:
+        roof["lds_busy_pmc"] = _r(rf["lds_busy_pmc"])
+    if "ceilings" in rf:
+        roof["lds_bank_conflict_ratio_pmc"] = _r(rf["ceilings"].get("lds_bank_conflict_ratio"))
+        roof["pmc_source"] = rf["ceilings"].get("source")
+    hb = rf.get("hbm", {})
+    roof["hbm"] = {"achieved": _r(hb.get("achieved")), "frac": _r(hb.get("frac")), "peak": hb.get("peak")}
+    tr = rf.get("triage", {})
+    roof["triage"] = {"kernel": tr.get("kernel"), "avg_launch_ms": _r(tr.get("avg_launch_ms")),
+                      "achieved": _r(tr.get("achieved")),
+                      "frac": _r(tr["achieved"] / HBM_PEAK_GBS) if tr.get("achieved") else None}
+    roof["ssf_kernel"] = rf.get("ssf_kernel")
+    roof["ssf_avg_launch_ms"] = _r(rf.get("ssf_avg_launch_ms"))
+    roof["isolated_step_ms"] = _r(rf.get("isolated_step_ms"))
+    line["roofline"] = roof
+    if "cpu_baseline" in full:
+        cb = full["cpu_baseline"]
+        line["cpu_baseline"] = {"value": _r(cb["value"]), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+                                "dtype": cb.get("dtype"), "sample": cb["sample"][:400]}
+    if "ler_overlap_all" in full:
+        line["ler_overlap_all"] = full["ler_overlap_all"]
+    ler = full.get("ler", {})
+    if ler:
+        rows = list(ler.values())
+        cur = {"p": [_r(float(k)) for k in ler], "shots": rows[0]["shots"], "failures": [r["failures"] for r in rows]}
+        if "cpu_f64" in rows[0]:
+            cur["cpu_f64_shots"] = rows[0]["cpu_f64"]["shots"]
+            cur["cpu_f64_failures"] = [r["cpu_f64"]["failures"] for r in rows]
+        for v in full.get("variants", []):
+            if v["dtype"] in rows[0]:
+                cur[v["dtype"] + "_failures"] = [r[v["dtype"]]["failures"] for r in rows]
+        line["ler"] = cur
+    if "variants" in full:
+        line["variants"] = [{"dtype": v["dtype"], "value": _r(v["value"], 6), "ms_per_step": _r(v["ms_per_step"], 5)}
+                            for v in full["variants"]]
+    if "sample_and_decode" in full:
+        line["sample_and_decode"] = _r(full["sample_and_decode"]["value"], 5)
+    cfgs = {}
+    if "c3_line" in full:
+        ls = full["c3_line"]["lines"]
+        cfgs["c3"] = {"dtype": "f64", "p": [x["p"] for x in ls], "shots_per_s": [_r(x["shots_per_s"]) for x in ls],
+                      "frac": [_r(x["roofline"]["frac"], 3) for x in ls], "bound": "lds",
+                      "ler": [_r(x["ler"], 3) for x in ls], "kernel": ls[0]["bp_kernel"] if ls else None}
+    if "c4_line" in full:
+        ls = full["c4_line"]["lines"]
+        for prec in sorted({x["precision"] for x in ls}):
+            sel = [x for x in ls if x["precision"] == prec]
+            cfgs["c4_" + prec] = {"p": [x["p"] for x in sel], "shots_per_s": [_r(x["shots_per_s"]) for x in sel],
+                                  "frac": [_r(x["roofline"]["frac"], 3) for x in sel],
+                                  "bound": sel[0]["roofline"]["bound"], "kernel": sel[0]["bp_kernel"]}
+    if "large_code_roofline" in full:
+        lc = full["large_code_roofline"]
+        ls = lc["lines"]
+        cfgs["c5"] = {"dtype": "f64", "p": [x["p"] for x in ls], "shots_per_s": [_r(x["shots_per_s"]) for x in ls],
+                      "frac": [_r(x["roofline"]["frac"], 3) for x in ls], "bound": "hbm",
+                      "traffic": [_r(x["roofline"]["traffic"]) for x in ls], "ler": [_r(x["ler"], 3) for x in ls],
+                      "kernel": lc["kernel"]}
+    if "reference_default" in full:
+        rd = full["reference_default"]
+        cfgs["reference_default"] = {"shots_per_s": _r(rd["shots_per_s"]), "ler": _r(rd["ler"], 3),
+                                     "kernel": rd["kernel"]}
+        if "cpu_baseline" in rd:
+            c = rd["cpu_baseline"]
+            cfgs["reference_default"]["cpu"] = {"value": _r(c["value"]), "cores": c["cores"],
+                                                "osd": c.get("osd_impl"),
+                                                "fail_flags_identical": c["fail_flags_identical"]}
+    if cfgs:
+        line["configs"] = cfgs
+    line["detail"] = detail
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -669,7 +849,13 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 code line (c4_line; rank 0, N=1 only)")
     ap.add_argument("--no-reference-default", action="store_true",
                     help="skip the reference-default bposd line (reference_default_line; rank 0, N=1 only)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="side file (relative to the repo root unless absolute) for the full record: per-point LER "
+                         "and roofline, every config line; the stdout line names it")
+    ap.add_argument("--no-c3", action="store_true", help="skip the config-3 line (c3_line; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
+    # diagnostic: decode without SSF (prices SSF inside the overlapped step)
+    ap.add_argument("--no-ssf-exp", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     args.iso_steps = max(1, min(args.iso_steps, args.steps))
 
@@ -779,7 +965,9 @@ def main():
         sd_elapsed = run.timed(decs, args.steps, run.streams[:1], sampler=decs[0], warm=False)
         sd = total_shots / sd_elapsed
 
-    large = c4 = refdef = None
+    large = c4 = refdef = c3 = None
+    if rank == 0 and world == 1 and not fake and not args.no_c3:
+        c3 = c3_line(dev)
     if rank == 0 and world == 1 and not fake and not args.no_large_code:
         large = large_code_roofline(dev)
     if rank == 0 and world == 1 and not fake and not args.no_c4:
@@ -790,7 +978,7 @@ def main():
     if rank == 0:
         value = total_shots / elapsed
         cpu = None
-        if not args.no_cpu_baseline and world == 1 and not fake:
+        if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(code, ps, args)
         ler = {}
         for pi, p in enumerate(ps):
@@ -871,6 +1059,8 @@ def main():
                             "shots_per_s": r[3] / r[2] if r[2] > 0 else None} for r in rank_rows]
         result["ranks_seen"] = len(rank_rows)
         result["roofline"] = roof
+        if c3 is not None:
+            result["c3_line"] = c3
         if large is not None:
             result["large_code_roofline"] = large
         if c4 is not None:
@@ -884,7 +1074,16 @@ def main():
             result["ler_overlap_all"] = {
                 "headline_vs_cpu_f64": all(r["overlaps_cpu_f64"] for r in ler.values()),
                 "variant_vs_cpu_f64": all(r[variant[0]]["overlaps_cpu_f64"] for r in ler.values()) if variant else None}
-        print(json.dumps(result))
+        detail = args.detail_out if os.path.isabs(args.detail_out) else os.path.join(REPO, args.detail_out)
+        try:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as fh:
+                json.dump(result, fh, indent=1)
+        except OSError as e:  # the line still goes out; it says where the detail is not
+            detail = f"unwritten ({e})"
+        if os.path.isabs(detail) and detail.startswith(REPO + os.sep):
+            detail = os.path.relpath(detail, REPO)
+        print(json.dumps(compact_line(result, detail)))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
