@@ -244,15 +244,17 @@ def cpu_baseline(code, ps, args):
     return res
 
 
-def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.002, 0.005)):
+def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005)):
     """HBM roofline of the genuinely HBM-bound path: BASELINE config 5 (PSL(2,16)
     Cayley-graph LP code, n = 53,040) at R = 1 spacetime syndromes (H_st
     48,960 x 130,560, E = 236,640), BP min-sum f64 max_iter 50 + fold + logical
     check on the slot-group kernel, whose messages stream through HBM.  Per p:
     one warmup launch, one timed launch (HIP events around the BP kernel on its
-    launch stream).  The first p (0.002) is a point where BP converges and the
-    code decodes (the line's headline); the last (0.005) is the worst case where
+    launch stream).  The low points (p = 0.0005, 0.001) are where BP converges
+    at R = 1 and the code decodes (k = 4080 logicals: at p = 0.002 the LER is
+    already 0.74, profiles/r06a); the last (0.005) is the worst case where
     every shot runs all 50 iterations (LER ~1), kept as the bandwidth figure.
+    The warmup launch decodes 2^13 shots (module load, scratch sizing).
     Algorithmic bytes = 32 B per edge per shot-iteration (f64 v2c read + c2v
     write in the check pass, c2v read + v2c write in the column pass) + the
     per-shot I/O (syndrome, readout, outputs)."""
@@ -286,7 +288,8 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.002, 0.005)):
         dec.set_priors(np.full(n, 2 * p / 3))
         for b in range(2):
             sampler.sample_storage_device(1, p, p, SEED, 100, b * shots, shots, syn[b], rd[b])
-        dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
+        warm = min(shots, 1 << 13)
+        dec.decode_device(warm, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
         torch.cuda.synchronize(dev)
         dec.set_timing(1)
         t0 = time.perf_counter()

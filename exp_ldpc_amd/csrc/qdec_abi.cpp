@@ -101,8 +101,11 @@ struct qd_graph {
     void* mws = nullptr;
     size_t mws_bytes = 0;
     size_t mws_failed = 0;  // smallest scratch size whose allocation failed (0: none)
+    uint64_t mws_capped_calls = 0;  // calls served the reduced scratch since the failure
     // kernel timing ring (qd_graph_set_timing): 3 events per decode call
-    std::vector<hipEvent_t> tev;  // 4 per call (record_ev)
+    // [0..3] around the launch's kernels (record_ev), [4] behind the copy of
+    // the compact-list counters (note_listed): kTimingEvents per call
+    std::vector<hipEvent_t> tev;
     int t_cap = 0, t_count = 0;
     // per timed call: compact-list length of a two-pass launch (summed segment
     // counters, copied into pinned memory behind the launch), -1 otherwise
@@ -133,6 +136,8 @@ struct qd_graph {
 };
 
 namespace {
+
+constexpr int kTimingEvents = 5;
 
 template <typename T>
 int drs() { return lds_stride<T, kDR>(); }
@@ -809,10 +814,13 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
     // capped after an allocation failure: a request at or above the size that
     // failed keeps the reduced scratch (the launch sizes its grid from the bytes
     // it gets) instead of draining and failing the same allocation every call
-    if (need > G->mws_bytes && G->mws && G->mws_failed && need >= G->mws_failed && G->mws_bytes >= floor) {
+    // (every 64th such call retries the full size: the memory may be free again)
+    if (need > G->mws_bytes && G->mws && G->mws_failed && need >= G->mws_failed && G->mws_bytes >= floor &&
+        ++G->mws_capped_calls % 64 != 0) {
         *bytes = G->mws_bytes;
         return G->mws;
     }
+    const size_t want = need;
     if (need > G->mws_bytes) {
         ws_drain(G);  // launches still in flight may use the old scratch
         if (G->mws) hip_check(hipFree(G->mws), "hipFree scratch");
@@ -822,7 +830,10 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
         // (the launch sizes its grid from the bytes it gets; results do not change)
         for (;;) {
             const hipError_t e = hipMalloc(&G->mws, need);
-            if (e == hipSuccess) break;
+            if (e == hipSuccess) {
+                if (need == want) G->mws_failed = 0;  // the full size fits again: no longer capped
+                break;
+            }
             (void)hipGetLastError();  // clear the sticky error before any launch checks it
             G->mws = nullptr;
             if (e != hipErrorOutOfMemory || need <= floor)
@@ -845,14 +856,18 @@ void note_kernels(qd_graph* G) {
 
 void attach_timing(qd_graph* G, DecodeArgs& a) {
     a.ev = nullptr;
-    if (G->t_cap > 0 && G->t_count < G->t_cap) a.ev = &G->tev[(size_t)4 * G->t_count++];
+    if (G->t_cap > 0 && G->t_count < G->t_cap) a.ev = &G->tev[(size_t)kTimingEvents * G->t_count++];
 }
 
 // after a timed launch: the compact list's length (the triage's segment
-// counters, one per 128-B line) into the call's pinned slot, on the BP stream
-void note_listed(qd_graph* G, const DecodeArgs& a, hipStream_t s) {
+// counters, one per 128-B line) into the call's pinned slot, on the BP stream,
+// with the call's event [4] behind the copy (read_timing_detail waits on it).
+// A split SSF stream waits for that event too, so the workspace chain, which
+// continues on the SSF stream, covers the copy: the next decode's triage never
+// resets the counters while the copy still reads them.
+void note_listed(qd_graph* G, const DecodeArgs& a, hipStream_t s, hipStream_t chain) {
     if (!a.ev || !G->t_listed) return;
-    const size_t slot = (size_t)(a.ev - G->tev.data()) / 4;
+    const size_t slot = (size_t)(a.ev - G->tev.data()) / kTimingEvents;
     const bool cmp = !G->last_pre.empty() && a.cmp_count;
     G->t_cmp[slot] = cmp ? 1 : 0;
     if (cmp)
@@ -860,9 +875,12 @@ void note_listed(qd_graph* G, const DecodeArgs& a, hipStream_t s) {
                                    kCmpLists * kCmpSegs,
                                    hipMemcpyDeviceToHost, s),
                   "hipMemcpy2DAsync list counters");
+    hip_check(hipEventRecord(a.ev[4], s), "hipEventRecord");
+    if (chain != s) hip_check(hipStreamWaitEvent(chain, a.ev[4], 0), "hipStreamWaitEvent");
 }
 
 void free_timing(qd_graph* G) {
+    ws_drain(G);  // list-counter copies into t_listed may still be in flight
     for (hipEvent_t e : G->tev) (void)hipEventDestroy(e);
     G->tev.clear();
     if (G->t_listed) (void)hipHostFree(G->t_listed);
@@ -1151,6 +1169,8 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->stream) (void)hipStreamSynchronize(g->stream);
         if (g->ws_ev_live) (void)hipEventSynchronize(g->ws_ev);
         if (g->ws_ev) (void)hipEventDestroy(g->ws_ev);
+        g->ws_ev = nullptr;
+        g->ws_ev_live = false;  // drained above (free_timing's drain is a no-op)
         if (g->ssf_ev) (void)hipEventDestroy(g->ssf_ev);
         g->arena.release();
         g->flip_arena.release();
@@ -1582,7 +1602,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
-        note_listed(G, a, s);
+        note_listed(G, a, s, split ? G->ssf_stream : s);
         // the last user of the queue is the SSF kernel: the workspace chain
         // continues on its stream (the next decode on this handle waits for it)
         ws_release(G, split ? G->ssf_stream : s);
@@ -1642,7 +1662,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
-        note_listed(G, a, s);
+        note_listed(G, a, s, s);
         ws_release(G, s);
         auto d2h = [&](void* h, const Reg& r, const char* what) {
             if (h) hip_check(hipMemcpyAsync(h, dptr(r), r.bytes, hipMemcpyDeviceToHost, s), what);
@@ -1745,7 +1765,7 @@ int qd_graph_set_timing(qd_graph* G, int32_t capacity) {
         set_device(G);
         if (capacity < 0) throw Fail(-90, "negative timing capacity");
         free_timing(G);
-        G->tev.resize((size_t)4 * capacity);
+        G->tev.resize((size_t)kTimingEvents * capacity);
         for (auto& e : G->tev) hip_check(hipEventCreate(&e), "hipEventCreate");
         if (capacity > 0) {
             void* h = nullptr;
@@ -1766,7 +1786,7 @@ int qd_graph_read_timing(qd_graph* G, float* bp_ms, float* ssf_ms, int32_t max_c
         if (!n_calls) throw Fail(-91, "null n_calls");
         const int n = std::min(G->t_count, std::max(0, max_calls));
         for (int i = 0; i < n; ++i) {
-            hipEvent_t* e = &G->tev[(size_t)4 * i];
+            hipEvent_t* e = &G->tev[(size_t)kTimingEvents * i];
             hip_check(hipEventSynchronize(e[2]), "hipEventSynchronize");
             float t0 = 0, t1 = 0;
             hip_check(hipEventElapsedTime(&t0, e[0], e[1]), "hipEventElapsedTime");
@@ -1787,9 +1807,10 @@ int qd_graph_read_timing_detail(qd_graph* G, float* pre_ms, float* bp_ms, float*
         if (!n_calls) throw Fail(-91, "null n_calls");
         const int n = std::min(G->t_count, std::max(0, max_calls));
         for (int i = 0; i < n; ++i) {
-            hipEvent_t* e = &G->tev[(size_t)4 * i];
+            hipEvent_t* e = &G->tev[(size_t)kTimingEvents * i];
             hip_check(hipEventSynchronize(e[2]), "hipEventSynchronize");
             hip_check(hipEventSynchronize(e[1]), "hipEventSynchronize");
+            if (G->t_cmp[i]) hip_check(hipEventSynchronize(e[4]), "hipEventSynchronize");
             float t0 = 0, t1 = 0, t2 = 0;
             hip_check(hipEventElapsedTime(&t0, e[0], e[3]), "hipEventElapsedTime");
             hip_check(hipEventElapsedTime(&t1, e[3], e[1]), "hipEventElapsedTime");
