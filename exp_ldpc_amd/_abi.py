@@ -90,10 +90,14 @@ SIGNATURES = {
     "qd_graph_hgp_set_slots": (_i32, [_p, _i32]),
     "qd_graph_hgp_source": (_i64, [_p, C.c_char_p, _i64]),
     "qd_graph_hgp_compile": (_i32, [_p]),
-    "qd_graph_hgp_replace_source": (_i32, [_p, C.c_char_p]),
     "qd_graph_hgp_decode_bp": (_i32, [_p, _i64, _p, _p, _p, _p, _i32, C.c_double, _p]),
     "qd_gf2_rref": (_i64, [_p, _i64, _i64, _i64, _p, _i32]),
     "qd_gf2_extend_basis": (_i64, [_p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64]),
+}
+
+# exported only by development builds (-DQDEC_DEV_HOOKS; not declared in include/qdec.h)
+DEV_SIGNATURES = {
+    "qd_graph_hgp_replace_source": (_i32, [_p, C.c_char_p]),
 }
 
 
@@ -116,8 +120,10 @@ def load(path: str | None = None) -> C.CDLL:
         raise QdecError(f"{p} not found: build it with `python -m exp_ldpc_amd.build` (hipcc, gfx950). "
                         "There is no CPU fallback for the decoder.")
     lib = C.CDLL(p)
-    for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+    for name, (res, args) in list(SIGNATURES.items()) + list(DEV_SIGNATURES.items()):
+        fn = getattr(lib, name, None)
+        if fn is None and name in DEV_SIGNATURES:
+            continue  # development hooks exist only in QDEC_DEV_HOOKS builds
         fn.restype = res
         fn.argtypes = args
     if lib.qd_abi_version() != 1:

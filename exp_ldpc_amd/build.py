@@ -30,7 +30,7 @@ ARCH = os.environ.get("QDEC_OFFLOAD_ARCH", "gfx950")
 FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
-    "-Wall", "-Wno-unused-result", "-pthread",
+    "-Wall", "-Wno-unused-result", "-pthread", f'-DQDEC_ARCH="{ARCH}"',
 ]
 
 

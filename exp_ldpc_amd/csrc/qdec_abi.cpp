@@ -1073,8 +1073,12 @@ int qd_graph_hgp_set_slots(qd_graph* G, int32_t slots) {
         if (slots < 0 || slots > 64) throw Fail(-95, "slots out of range");
         if (!G->host_only) set_device(G);
         if (G->stream) hip_check(hipStreamSynchronize(G->stream), "hipStreamSynchronize");
+        ws_drain(G);  // an HGP launch on another stream may still use the plan's module
+        HgpPlan* P = hgp_plan_create(G->dg.m, G->dg.n, G->row_ptr, G->col_idx, slots);
+        if (!P && slots > 0 && hgp_plan_of(G))  // a hypergraph product, but no feasible plan with `slots`
+            throw Fail(-95, "no feasible HGP plan with this many slots per workgroup");
         hgp_plan_destroy(G->hgp);
-        G->hgp = hgp_plan_create(G->dg.m, G->dg.n, G->row_ptr, G->col_idx, slots);
+        G->hgp = P;
         G->hgp_tried = true;
     });
 }
@@ -1107,6 +1111,9 @@ int64_t qd_graph_hgp_source(qd_graph* G, char* buf, int64_t cap) {
     return e ? e : len;
 }
 
+#ifdef QDEC_DEV_HOOKS
+// development build only (python -m exp_ldpc_amd.build --tag dev -DQDEC_DEV_HOOKS):
+// compile an edited kernel source at run time (tools/gpu/hgp_debug.py)
 int qd_graph_hgp_replace_source(qd_graph* G, const char* src) {
     return guarded([&] {
         check_graph(G);
@@ -1116,6 +1123,7 @@ int qd_graph_hgp_replace_source(qd_graph* G, const char* src) {
         hgp_plan_replace_source(P, src);
     });
 }
+#endif
 
 int qd_graph_hgp_compile(qd_graph* G) {
     return guarded([&] {
@@ -1123,7 +1131,8 @@ int qd_graph_hgp_compile(qd_graph* G) {
         HgpPlan* P = hgp_plan_of(G);
         if (!P) throw Fail(-90, "not a hypergraph-product check matrix");
         std::string log;
-        if (hgp_plan_compile(P, "gfx950", &log) != 0) throw Fail(-91, "HGP kernel compile failed: " + log);
+        if (hgp_plan_compile(P, hgp_target_arch(G->host_only ? -1 : G->device).c_str(), &log) != 0)
+            throw Fail(-91, "HGP kernel compile failed: " + log);
     });
 }
 
@@ -1137,7 +1146,8 @@ int qd_graph_hgp_decode_bp(qd_graph* G, int64_t B, const uint8_t* syn, uint8_t* 
         if (!P) throw Fail(-90, "not a hypergraph-product check matrix");
         if (!G->has_priors) throw Fail(-51, "priors not set");
         if (B < 0 || (B > 0 && !syn) || max_iter < 1) throw Fail(-92, "invalid HGP decode arguments");
-        if (hgp_plan_load(P, G->num_cus) != 0) throw Fail(-93, "HGP kernel load failed");
+        if (hgp_plan_load(P, G->num_cus, hgp_target_arch(G->device).c_str()) != 0)
+            throw Fail(-93, "HGP kernel load failed");
         if (!G->ctl) hip_check(hipMalloc(&G->ctl, 256), "hipMalloc control block");
         if (B == 0) return;
         HgpBpArgs a{};
@@ -1146,13 +1156,17 @@ int qd_graph_hgp_decode_bp(qd_graph* G, int64_t B, const uint8_t* syn, uint8_t* 
         a.x_out = x_out;
         a.iters = iters;
         a.status = status;
-        a.counter = static_cast<unsigned long long*>(G->ctl) + 1;
+        // its own shot counter on its own 128-B line (words 0 / 1 are the BP and
+        // SSF kernels' counters), and inside the workspace chain like every decode
+        a.counter = static_cast<unsigned long long*>(G->ctl) + 16;
         a.B = B;
         a.max_iter = max_iter;
         a.ms_scaling = ms_scaling;
         hipStream_t st = stream ? static_cast<hipStream_t>(stream) : G->stream;
+        ws_acquire(G, st);
         if (hgp_launch_bp(P, a, st) != 0) throw Fail(-94, "HGP kernel launch failed");
         hip_check(hipGetLastError(), "HGP kernel");
+        ws_release(G, st);
     });
 }
 

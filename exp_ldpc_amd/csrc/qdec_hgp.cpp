@@ -153,6 +153,10 @@ HgpPlan* hgp_plan_create(int m, int n, const std::vector<int32_t>& rp, const std
         const double used = (double)per_cu * S * (P->a0 + P->b0);
         if (slots > 0 ? S == slots : used > best * 1.0001) best = used, bestS = S, bestW = WL;
     }
+    if (bestS == 0) {  // `slots` (or every S) fits no workgroup: no plan
+        delete P;
+        return nullptr;
+    }
     P->S = bestS;
     P->WL = bestW;
     P->WR = (bestS * P->b0 + 63) / 64;
@@ -174,7 +178,7 @@ void hgp_plan_destroy(HgpPlan* P) {
 
 const std::string& hgp_plan_source(const HgpPlan* P) { return P->src; }
 
-// development: run an edited source (tools/dev, kernel debugging)
+// development: run an edited source (QDEC_DEV_HOOKS builds, kernel debugging)
 void hgp_plan_replace_source(HgpPlan* P, const std::string& src) {
     if (P->mod) (void)hipModuleUnload(P->mod);
     P->mod = nullptr;
@@ -225,11 +229,11 @@ int hgp_plan_compile(HgpPlan* P, const char* arch, std::string* log) {
 }
 
 // compile (if needed) and load on the current device
-int hgp_plan_load(HgpPlan* P, int num_cus) {
+int hgp_plan_load(HgpPlan* P, int num_cus, const char* arch) {
     if (P->fn) return 0;
     if (P->code.empty()) {
         std::string log;
-        if (int rc = hgp_plan_compile(P, "gfx950", &log)) {
+        if (int rc = hgp_plan_compile(P, arch, &log)) {
             std::fprintf(stderr, "qdec: HGP kernel compile failed (%d):\n%s\n", rc, log.c_str());
             return rc;
         }
@@ -255,6 +259,21 @@ int hgp_launch_bp(HgpPlan* P, const HgpBpArgs& args, hipStream_t stream) {
     const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(P->grid, need));
     if (hipModuleLaunchKernel(P->fn, grid, 1, 1, threads, 1, 1, 0, stream, params, nullptr) != hipSuccess) return -8;
     return 0;
+}
+
+// the hipRTC target: the device's own gfx name without its feature suffix
+// (gcnArchName "gfx950:sramecc+:xnack-" -> "gfx950"); device < 0 (host-only
+// handles) or no device: the architecture the library itself was built for
+std::string hgp_target_arch(int device) {
+    if (device >= 0) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.gcnArchName[0]) {
+            std::string a(prop.gcnArchName);
+            return a.substr(0, a.find(':'));
+        }
+        (void)hipGetLastError();
+    }
+    return QDEC_ARCH;
 }
 
 void hgp_plan_info(const HgpPlan* P, int* out8) {

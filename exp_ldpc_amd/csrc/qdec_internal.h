@@ -353,7 +353,8 @@ void hgp_plan_destroy(HgpPlan* P);
 const std::string& hgp_plan_source(const HgpPlan* P);
 void hgp_plan_replace_source(HgpPlan* P, const std::string& src);  // development
 int hgp_plan_compile(HgpPlan* P, const char* arch, std::string* log);  // hipRTC (no device needed)
-int hgp_plan_load(HgpPlan* P, int num_cus);                              // compile + load on the current device
+int hgp_plan_load(HgpPlan* P, int num_cus, const char* arch);           // compile + load on the current device
+std::string hgp_target_arch(int device);  // hipRTC target of `device` (< 0: the build's QDEC_ARCH)
 int hgp_launch_bp(HgpPlan* P, const HgpBpArgs& a, hipStream_t stream);
 void hgp_plan_info(const HgpPlan* P, int* out8);  // a0 a1 b0 b1 S WL WR per_cu
 

@@ -302,12 +302,14 @@ int qd_graph_ssf_tables_copy(const qd_graph* g, uint32_t* lut, uint32_t* off, ui
  * qd_graph_hgp_compile: compile only (no device needed).  No reference
  * counterpart (the reference decodes with ldpc's generic BpDecoder). */
 int qd_graph_hgp_info(qd_graph* g, int32_t* out8);
-/* Re-plan with `slots` shot slots per workgroup (0: the library's choice). */
+/* Re-plan with `slots` shot slots per workgroup (0: the library's choice);
+ * -95 when no workgroup shape holds `slots` (the previous plan stays). */
 int qd_graph_hgp_set_slots(qd_graph* g, int32_t slots);
 int64_t qd_graph_hgp_source(qd_graph* g, char* buf, int64_t cap);
 int qd_graph_hgp_compile(qd_graph* g);
-/* Development: replace the generated source (kernel debugging, tools/dev). */
-int qd_graph_hgp_replace_source(qd_graph* g, const char* src);
+/* (Development builds with -DQDEC_DEV_HOOKS also export
+ * qd_graph_hgp_replace_source(g, src), which recompiles an edited kernel
+ * source; the product library does not.) */
 /* BP only (f64 min-sum, ldpc v1 semantics as qd_decode_batch_device with
  * method QD_MIN_SUM, precision QD_F64, no SSF): device buffers syn [B][m],
  * x_out [B][n] (or null), iters [B], status [B] (bit 0: converged). */

@@ -592,6 +592,13 @@ def test_hgp_kernel_plan_and_rtc_compile(code225):
     assert np.array_equal(A.T, B)  # biregular_hgp: B = A^T
     assert [sum(Arm[x] >> w & 1 for w in range(a1)) for x in range(a0)] == list(np.diff(Arp))
     _abi.check(lib.qd_graph_hgp_compile(h), "hgp compile")  # hipRTC, no device
+    # a slot count no workgroup shape holds (2 x 64 x 108 x 16 B of LDS states
+    # alone) is refused and the previous plan stays; a feasible one re-plans
+    assert lib.qd_graph_hgp_set_slots(h, 64) == -95
+    assert lib.qd_graph_hgp_info(h, info) == 1 and list(info)[4] == S
+    _abi.check(lib.qd_graph_hgp_set_slots(h, 2), "hgp slots")
+    assert lib.qd_graph_hgp_info(h, info) == 1 and list(info)[4] == 2
+    assert not hasattr(lib, "qd_graph_hgp_replace_source")  # development builds only
     lib.qd_graph_destroy(h)
     # not hypergraph products
     rng = np.random.default_rng(3)

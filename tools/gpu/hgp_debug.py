@@ -1,4 +1,8 @@
-"""Debug the HGP kernel on the GPU with device printf in an edited source."""
+"""Debug the HGP kernel on the GPU with device printf in an edited source.
+
+Needs the development build (qd_graph_hgp_replace_source):
+  python -m exp_ldpc_amd.build --tag dev -DQDEC_DEV_HOOKS
+  QDEC_LIB=exp_ldpc_amd/libqdec_hip_dev.so python tools/gpu/hgp_debug.py"""
 import ctypes as C
 import os
 import sys
