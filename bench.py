@@ -490,7 +490,7 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
 
 
 def reference_default_line(dev, code, shots: int = 1 << 18, batch: int = 1 << 16, p: float = 0.01,
-                           cpu_shots: int = 10000, cpu: bool = True):
+                           cpu_shots: int = 1 << 16, cpu: bool = True):
     """The reference's own default decode (BASELINE configs[0]: scripts/p_sweep.py
     -> misc/p_sweep.py:57-78 defaults, _experiment.py:62-83,213-229): R = 1,
     decoder_mode bposd, product-sum BP, max_iter = n = 225, OSD-CS order 7,
@@ -500,9 +500,10 @@ def reference_default_line(dev, code, shots: int = 1 << 18, batch: int = 1 << 16
     device-sampled shots in `batch`-shot runs; BP time from the BP decoder's HIP
     events, OSD + the rest = the remainder.  CPU leg: the oracle's restatement of
     the same loop (oracle/harness_py.spacetime_bposd_corrections: the C ldpc-v1
-    BP restatement on 16 host threads + the numpy OSD restatement) on the first
-    `cpu_shots` of the same syndromes, BP and OSD timed apart, failure flags
-    compared shot by shot."""
+    BP restatement + the C OSD restatement, both OpenMP over shots on the host's
+    cores; a few OSD results re-checked against the numpy restatement, untimed)
+    on the first `cpu_shots` of the same syndromes, BP and OSD timed apart,
+    failure flags compared shot by shot."""
     import torch
     from exp_ldpc_amd.experiment import BatchPipeline
     from exp_ldpc_amd.noise_model import depolarizing_noise
@@ -552,15 +553,19 @@ def reference_default_line(dev, code, shots: int = 1 << 18, batch: int = 1 << 16
         x = out["x"].copy()
         bad = np.nonzero((out["status"] & 1) == 0)[0]
         t0 = time.perf_counter()
-        for b in bad:
-            x[b] = osd_decode(Hst, syn_h[b], out["llr"][b], "osd_cs", 7)[1]
+        if bad.size:  # compiled OSD-CS 7 (oracle/osd_impl.inc, OpenMP over the BP failures)
+            x[bad] = orc.osd(Hst, syn_h[bad], out["llr"][bad], "osd_cs", 7, nthreads=threads)[1]
         t_osd = time.perf_counter() - t0
+        # spot check of the compiled OSD against the numpy restatement (untimed)
+        for b in bad[:8]:
+            assert np.array_equal(x[b], osd_decode(Hst, syn_h[b], out["llr"][b], "osd_cs", 7)[1])
         corr = _fold(x, code.checks.z.shape[1], R)
         cpu_fail = logical_failures(code.logicals.z, rd_h, corr)
         res["cpu_baseline"] = {"value": cpu_shots / (t_bp + t_osd), "unit": "shots/s", "cores": threads, "kind": "port",
                                "sample": f"the first {cpu_shots} of the GPU run's shots; oracle BP (C, OpenMP) "
-                                         f"{t_bp:.2f} s + numpy OSD-CS 7 on {bad.size} BP failures {t_osd:.2f} s",
-                               "bp_s": t_bp, "osd_s": t_osd,
+                                         f"{t_bp:.2f} s + compiled OSD-CS 7 (C, OpenMP) on {bad.size} BP failures "
+                                         f"{t_osd:.3f} s",
+                               "bp_s": t_bp, "osd_s": t_osd, "osd_impl": "C (oracle/osd_impl.inc), OpenMP",
                                "fail_flags_identical": bool(np.array_equal(cpu_fail, first.fail[:cpu_shots]))}
     del batches, pipe
     torch.cuda.empty_cache()

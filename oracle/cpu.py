@@ -41,6 +41,9 @@ class OracleLib:
         ph = self.lib.qdo_philox4x32_10
         ph.restype = None
         ph.argtypes = [_p, _p, _p]
+        o = self.lib.qdo_osd_batch
+        o.restype = _i32
+        o.argtypes = [_i32, _i32, _p, _p, _i64, _p, _p, _i32, _i32, _p, _p, _i32]
         th = self.lib.qdo_threshold
         th.restype = C.c_uint32
         th.argtypes = [C.c_double]
@@ -121,6 +124,26 @@ class OracleLib:
         if rc != 0:
             raise ValueError(f"qdo_sample_storage failed with status {rc}")
         return syn, rd
+
+    def osd(self, H, syn, llr, method="osd_cs", order=0, nthreads=0):
+        """Compiled OSD (osd_impl.inc) of a batch: returns (osd0, osdw) uint8[B][n]."""
+        import scipy.sparse as sp
+        H = sp.csr_matrix(H)
+        H.sort_indices()
+        m, n = H.shape
+        syn = np.ascontiguousarray(np.asarray(syn, dtype=np.uint8).reshape(-1, m))
+        B = syn.shape[0]
+        llr = np.ascontiguousarray(np.asarray(llr, dtype=np.float64).reshape(B, n))
+        rp = np.ascontiguousarray(H.indptr, dtype=np.int32)
+        ci = np.ascontiguousarray(H.indices, dtype=np.int32)
+        o0 = np.zeros((B, n), np.uint8)
+        ow = np.zeros((B, n), np.uint8)
+        rc = self.lib.qdo_osd_batch(m, n, _ptr(rp), _ptr(ci), int(B), _ptr(syn), _ptr(llr),
+                                    {"osd0": 0, "osd_e": 1, "osd_cs": 2}[method], int(order), _ptr(o0), _ptr(ow),
+                                    int(nthreads))
+        if rc != 0:
+            raise ValueError(f"qdo_osd_batch failed with status {rc}")
+        return o0, ow
 
     def philox(self, ctr, key):
         c = np.ascontiguousarray(ctr, dtype=np.uint32)

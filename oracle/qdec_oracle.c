@@ -420,3 +420,6 @@ int qdo_sample_storage(int32_t m, int32_t n, const int32_t* row_ptr, const int32
     }
     return 0;
 }
+
+/* ---- OSD (bposd post-processing; the reference-default CPU leg) ---- */
+#include "osd_impl.inc"

@@ -63,6 +63,14 @@ int qdo_sample_storage(int32_t m, int32_t n, const int32_t* row_ptr, const int32
                        uint32_t seed, uint32_t stream, int64_t shot0, int64_t B,
                        uint8_t* syn, uint8_t* readout, int32_t nthreads);
 
+/* OSD of B shots from their BP soft output (oracle/osd_impl.inc; same spec as
+ * oracle/osd_py.py and the product's qd_osd_batch): method 0 osd0, 1 osd_e,
+ * 2 osd_cs; llr[B][n] double; osd0 / osdw [B][n] (either may be NULL).
+ * OpenMP over shots. */
+int qdo_osd_batch(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx, int64_t B,
+                  const uint8_t* syn, const double* llr, int32_t method, int32_t order, uint8_t* osd0,
+                  uint8_t* osdw, int32_t nthreads);
+
 /* Raw Philox4x32-10 block (exposed for known-answer tests). */
 void qdo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

@@ -224,3 +224,30 @@ def test_sampler_schedule_matches_reference_circuit(R):
     assert _parse_schedule(text) == _sampler_schedule(R)
     # noise parameters as written by depolarizing_noise(0.01, 0.01)
     assert "DEPOLARIZE1(0.01)" in text and "MZ(0.01)" in text
+
+
+@pytest.mark.parametrize("method,order", [("osd0", 0), ("osd_e", 4), ("osd_cs", 7), ("osd_cs", 0)])
+def test_compiled_osd_equals_numpy_restatement(oracle_lib, method, order):
+    """oracle/osd_impl.inc (the reference-default CPU leg's OSD) against the
+    independent numpy restatement oracle/osd_py.py, bit for bit: on the R = 1
+    spacetime matrix of the n = 225 code (216 x 558, the bench's graph) with BP
+    soft outputs, and on a rank-deficient random matrix with quantised llr
+    (exact ties: the stable order decides)."""
+    from oracle.harness_py import _spacetime_matrix
+    from oracle.osd_py import osd_decode
+    rng = np.random.default_rng(11)
+    Hst, prior = _spacetime_matrix(HZ, 1, 0.02, 0.02)
+    Hst = sp.csr_matrix(Hst)
+    e = (rng.random((10, Hst.shape[1])) < 0.03).astype(np.uint8)
+    syn = ((Hst @ e.T).T % 2).astype(np.uint8)
+    out = oracle_lib.decode(Hst, prior, syn, method="ps", precision="f64", max_iter=8, want_llr=True)
+    cases = [(Hst, syn, out["llr"])]
+    R = sp.csr_matrix((rng.random((40, 70)) < 0.08).astype(np.uint8))
+    R = sp.vstack([R, R[:3]]).tocsr()  # dependent rows
+    e2 = (rng.random((12, 70)) < 0.1).astype(np.uint8)
+    cases.append((R, ((R @ e2.T).T % 2).astype(np.uint8), np.round(rng.normal(size=(12, 70)), 0)))
+    for H, s, llr in cases:
+        o0, ow = oracle_lib.osd(H, s, llr, method, order, nthreads=3)
+        for b in range(s.shape[0]):
+            r0, rw = osd_decode(H, s[b], llr[b], method, order)
+            assert np.array_equal(o0[b], r0) and np.array_equal(ow[b], rw), (method, order, b)
