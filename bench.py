@@ -82,8 +82,14 @@ CODE = "hgp_12_3_4_s1234"
 SEED = 20250221
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b64/b128 rate, every CU streaming (MI355X_MICROARCH.md §LDS)
-IO_BYTES_PER_SHOT = 108 + 225 + 1 + 1 + 4  # syndrome + readout in; fail, status, iters out
-TRIAGE_BYTES_PER_SHOT = 108 + 225  # the triage reads each shot's syndrome and readout rows
+OUT_BYTES_PER_SHOT = 1 + 1 + 4  # fail, status, iters out
+
+
+def in_bytes_per_shot(m: int, n: int, packed: bool) -> int:
+    """Input bytes the triage reads per shot: the syndrome and readout rows, as
+    bytes (m + n) or as bit-packed u64 words (QD_INPUT_PACKED: 8 ceil(m/64) +
+    8 ceil(n/64); 16 + 32 = 48 B at n = 225 instead of 333)."""
+    return 8 * ((m + 63) // 64 + (n + 63) // 64) if packed else m + n
 
 
 def wilson(k: int, n: int, z: float = 1.96):
@@ -145,15 +151,17 @@ def lds_roofline(bp_ms, pre_ms, listed, it_iso, args, hz, bp_kernel, ssf_kernel,
     per launch and per sweep point."""
     E, m = int(hz.nnz), int(hz.shape[0])
     lds_per_it = 32 * E + 16 * m
+    tri_shot = in_bytes_per_shot(m, int(hz.shape[1]), args.inputs == "packed")
+    io_shot = tri_shot + OUT_BYTES_PER_SHOT
     B = args.batch
     it_bp = np.where(listed >= 0, it_iso - (B - listed), it_iso).astype(np.float64)
     stage_ms = bp_ms + pre_ms
     tot_ms = float(bp_ms.sum())
     lds_bytes = float(lds_per_it * it_bp.sum())
     achieved = lds_bytes / (tot_ms * 1e-3) / 1e9
-    io_launch = IO_BYTES_PER_SHOT * B
+    io_launch = io_shot * B
     hbm_ach = io_launch / (stage_ms.mean() * 1e-3) / 1e9
-    tri_bytes = TRIAGE_BYTES_PER_SHOT * B
+    tri_bytes = tri_shot * B
     per_point = {}
     for pi in range(bp_ms.shape[1]):
         ms = float(bp_ms[:, pi].mean())
@@ -174,13 +182,13 @@ def lds_roofline(bp_ms, pre_ms, listed, it_iso, args, hz, bp_kernel, ssf_kernel,
                            "(sum(iters) - (B - listed))",
             "hbm": {"achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": io_launch,
-                    "bytes_model": f"per shot {IO_BYTES_PER_SHOT} B compulsory HBM I/O (108 B syndrome + 225 B "
-                                   "readout in, fail + status + int32 iterations out) over the BP stage (triage + "
-                                   "BP kernel)"},
+                    "bytes_model": f"per shot {io_shot} B compulsory HBM I/O ({tri_shot} B of syndrome + "
+                                   f"readout rows in ({args.inputs}), fail + status + int32 iterations out) over "
+                                   "the BP stage (triage + BP kernel)"},
             "triage": {"avg_launch_ms": float(pre_ms.mean()),
                        "achieved": tri_bytes / (float(pre_ms.mean()) * 1e-3) / 1e9 if pre_ms.mean() > 0 else None,
                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "bytes_model": f"{TRIAGE_BYTES_PER_SHOT} B per shot: syndrome + readout rows read once"},
+                       "bytes_model": f"{tri_shot} B per shot: syndrome + readout rows ({args.inputs}) read once"},
             "per_point": per_point,
             "ssf_kernel": ssf_kernel, "ssf_avg_launch_ms": float(ssf_ms.mean()),
             "isolated_step_ms": float(stage_ms.sum(axis=1).mean() + ssf_ms.sum(axis=1).mean())}
@@ -324,7 +332,7 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005)):
     return res
 
 
-def c3_line(dev, shots: int = 1 << 22, ps=(0.001, 0.003, 0.01), precision: str = "f64"):
+def c3_line(dev, shots: int = 1 << 22, ps=(0.001, 0.003, 0.01), precision: str = "f64", packed: bool = True):
     """BASELINE config 3 on one GPU: the [[144,12,12]] bivariate-bicycle lift
     (quasi-cyclic lifted product over Z_12 x Z_6, built by
     exp_ldpc_amd.lifted.bivariate_bicycle_code; reference construction
@@ -343,8 +351,12 @@ def c3_line(dev, shots: int = 1 << 22, ps=(0.001, 0.003, 0.01), precision: str =
     m, n = hz.shape
     E = int(hz.nnz)
     lds_per_it = 32 * E + 16 * m
-    syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
-    rd = torch.empty((2, shots, n), dtype=torch.uint8, device=dev)
+    if packed:
+        syn = torch.empty((2, shots, (m + 63) // 64), dtype=torch.int64, device=dev)
+        rd = torch.empty((2, shots, (n + 63) // 64), dtype=torch.int64, device=dev)
+    else:
+        syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
+        rd = torch.empty((2, shots, n), dtype=torch.uint8, device=dev)
     iters = torch.empty((2, shots), dtype=torch.int32, device=dev)
     status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
     fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
@@ -354,14 +366,14 @@ def c3_line(dev, shots: int = 1 << 22, ps=(0.001, 0.003, 0.01), precision: str =
         dec = Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0, flip_sets=hx,
                       logicals=lz, device=dev.index)
         for b in range(2):
-            dec.sample_storage_device(0, p, p, SEED, 400, b * shots, shots, syn[b], rd[b])
+            dec.sample_storage_device(0, p, p, SEED, 400, b * shots, shots, syn[b], rd[b], packed=packed)
         dec.decode_device(shots, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0],
-                          ssf_steps=steps[0])
+                          ssf_steps=steps[0], packed=packed)
         torch.cuda.synchronize(dev)
         dec.set_timing(1)
         t0 = time.perf_counter()
         dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1],
-                          ssf_steps=steps[1])
+                          ssf_steps=steps[1], packed=packed)
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         pre_ms, bp_ms, ssf_ms, listed = dec.read_timing_detail()
@@ -379,8 +391,8 @@ def c3_line(dev, shots: int = 1 << 22, ps=(0.001, 0.003, 0.01), precision: str =
                       "roofline": {"bound": "lds", "achieved": ach, "peak": LDS_PEAK_GBS, "unit": "GB/s",
                                    "frac": ach / LDS_PEAK_GBS, "traffic": None,
                                    "algorithmic_bytes_per_launch": lds_per_it * it_bp},
-                      "hbm_frac_bp_stage": shots * (m + n + 6) / ((float(pre_ms[0]) + float(bp_ms[0])) * 1e-3) / 1e9
-                      / HBM_PEAK_GBS})
+                      "hbm_frac_bp_stage": shots * (in_bytes_per_shot(m, n, packed) + OUT_BYTES_PER_SHOT)
+                      / ((float(pre_ms[0]) + float(bp_ms[0])) * 1e-3) / 1e9 / HBM_PEAK_GBS})
         del dec
     del syn, rd
     torch.cuda.empty_cache()
@@ -579,7 +591,7 @@ class FakeDecoder:
     def __init__(self, dev):
         self.dev = dev
 
-    def sample_storage_device(self, rounds, p_data, p_meas, seed, stream_id, shot0, B, syn, readout, stream=None):
+    def sample_storage_device(self, rounds, p_data, p_meas, seed, stream_id, shot0, B, syn, readout, stream=None, **_):
         import torch
         syn.copy_(((torch.arange(shot0, shot0 + B, device=self.dev)[:, None] + stream_id) % 2).to(torch.uint8))
         readout.zero_()
@@ -614,8 +626,15 @@ class Run:
         self.nsteps = args.warmup + args.steps
         P = len(ps)
         u8 = dict(dtype=torch.uint8, device=dev)
-        self.syn = torch.empty((self.nsteps, P, self.B, m), **u8)
-        self.rd = torch.empty((self.nsteps, P, self.B, n), **u8)
+        # inputs as byte rows or bit-packed u64 rows (--inputs; QD_INPUT_PACKED)
+        self.packed = args.inputs == "packed"
+        if self.packed:
+            w = dict(dtype=torch.int64, device=dev)
+            self.syn = torch.empty((self.nsteps, P, self.B, (m + 63) // 64), **w)
+            self.rd = torch.empty((self.nsteps, P, self.B, (n + 63) // 64), **w)
+        else:
+            self.syn = torch.empty((self.nsteps, P, self.B, m), **u8)
+            self.rd = torch.empty((self.nsteps, P, self.B, n), **u8)
         self.iters = torch.empty((self.nsteps, P, self.B), dtype=torch.int32, device=dev)
         self.status = torch.empty((self.nsteps, P, self.B), **u8)
         self.fail = torch.empty((self.nsteps, P, self.B), **u8)
@@ -636,7 +655,7 @@ class Run:
     def sample(self, sampler, s, stream=None):
         for pi, p in enumerate(self.ps):
             sampler.sample_storage_device(0, p, p, SEED, pi, self.shot0(s), self.B, self.syn[s, pi], self.rd[s, pi],
-                                          **({} if stream is None else {"stream": stream}))
+                                          packed=self.packed, **({} if stream is None else {"stream": stream}))
 
     def sync(self):
         if not self.fake:
@@ -660,7 +679,7 @@ class Run:
             for pi in range(len(self.ps)):
                 decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                        status=self.status[s, pi], fail=self.fail[s, pi],
-                                       ssf_steps=self.ssf_steps[s, pi], ssf=self.ssf, stream=streams[0].cuda_stream)
+                                       ssf_steps=self.ssf_steps[s, pi], ssf=self.ssf, packed=self.packed, stream=streams[0].cuda_stream)
             ev = torch.cuda.Event()
             ev.record(self.ssf_stream)
             streams[0].wait_event(ev)
@@ -669,7 +688,7 @@ class Run:
             for pi in range(len(self.ps)):
                 decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                        status=self.status[s, pi], fail=self.fail[s, pi],
-                                       ssf_steps=self.ssf_steps[s, pi], ssf=self.ssf,
+                                       ssf_steps=self.ssf_steps[s, pi], ssf=self.ssf, packed=self.packed,
                                        **({} if self.fake else {"stream": streams[0].cuda_stream}))
             return
         join = self.args.step_join == "step"
@@ -683,7 +702,7 @@ class Run:
             st = streams[j % len(streams)]
             decs[pi].decode_device(self.B, syn=self.syn[s, pi], readout=self.rd[s, pi], iters=self.iters[s, pi],
                                    status=self.status[s, pi], fail=self.fail[s, pi], ssf_steps=self.ssf_steps[s, pi],
-                                   ssf=self.ssf, stream=st.cuda_stream)
+                                   ssf=self.ssf, packed=self.packed, stream=st.cuda_stream)
         if join:
             for st in streams[1:]:
                 e2 = torch.cuda.Event()
@@ -742,7 +761,8 @@ def compact_line(full: dict, detail: str) -> dict:
     line["value"] = _r(line["value"], 6)
     line["ms_per_step"] = _r(line["ms_per_step"], 6)
     cfg = full["config"]
-    line["config"] = {k: cfg[k] for k in ("workload", "shots_per_point_per_step_per_gpu", "global_batch", "parallelism")}
+    line["config"] = {k: cfg[k] for k in ("workload", "shots_per_point_per_step_per_gpu", "global_batch", "parallelism",
+                                          "inputs") if k in cfg}
     line["ranks_seen"] = full["ranks_seen"]
     line["ranks"] = [{"rank": x["rank"], "device": x["device"], "timed_s": _r(x["timed_s"], 6), "shots": x["shots"]}
                      for x in full["ranks"]][:16]
@@ -857,6 +877,9 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 code line (c4_line; rank 0, N=1 only)")
     ap.add_argument("--no-reference-default", action="store_true",
                     help="skip the reference-default bposd line (reference_default_line; rank 0, N=1 only)")
+    ap.add_argument("--inputs", default="packed", choices=["packed", "bytes"],
+                    help="device input rows: bit-packed u64 words (QD_INPUT_PACKED; the sampler writes them) or one "
+                         "byte per bit")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="side file (relative to the repo root unless absolute) for the full record: per-point LER "
                          "and roofline, every config line; the stdout line names it")
@@ -975,7 +998,7 @@ def main():
 
     large = c4 = refdef = c3 = None
     if rank == 0 and world == 1 and not fake and not args.no_c3:
-        c3 = c3_line(dev)
+        c3 = c3_line(dev, packed=args.inputs == "packed")
     if rank == 0 and world == 1 and not fake and not args.no_large_code:
         large = large_code_roofline(dev)
     if rank == 0 and world == 1 and not fake and not args.no_c4:
@@ -1049,6 +1072,7 @@ def main():
                                    "alpha_t=1-2^-t + SSF (Hx flip sets) + fused logical check",
                        "shots_per_point_per_step_per_gpu": args.batch, "global_batch": args.batch * P * world,
                        "parallelism": f"shot-sharded x{world}, no collective",
+                       "inputs": "bit-packed u64 rows (QD_INPUT_PACKED)" if args.inputs == "packed" else "byte rows",
                        "schedule": args.schedule if args.schedule == "pipeline" else
                        f"{args.streams} streams, joined {'every step' if args.step_join == 'step' else 'at the end'}",
                        "wave_waves_per_cu": {k: (v or "default") for k, v in occ.items()}},

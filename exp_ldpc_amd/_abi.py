@@ -25,6 +25,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "qdec.h")
 QD_PRODUCT_SUM, QD_MIN_SUM = 0, 1
 QD_F64, QD_F32 = 0, 1
 QD_SYN_ADD_BASE, QD_SYN_ADD_READOUT = 1, 2
+QD_INPUT_PACKED = 16  # bit-packed input rows (include/qdec.h)
 QD_ST_BP_CONVERGED, QD_ST_SATISFIED = 1, 2
 
 
@@ -69,6 +70,8 @@ SIGNATURES = {
     "qd_decode_batch": (_i32, [_p, C.POINTER(QdParams), _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "qd_decode_batch_device": (_i32, [_p, C.POINTER(QdParams), _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "qd_sample_storage_device": (_i32, [_p, _i32, C.c_double, C.c_double, _u32, _u32, _i64, _i64, _p, _p, _p]),
+    "qd_sample_storage_packed_device": (_i32, [_p, _i32, C.c_double, C.c_double, _u32, _u32, _i64, _i64, _p, _p,
+                                               _p]),
     "qd_count_flags_device": (_i32, [_p, _i64, C.c_uint8, _p, _p]),
     "qd_osd_batch": (_i32, [_i32, _i32, _p, _p, _i32, _i32, _i64, _p, _p, _p, _p, _i32]),
     "qd_osd_last_error": (C.c_char_p, []),

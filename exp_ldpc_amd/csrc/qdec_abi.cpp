@@ -100,6 +100,10 @@ struct qd_graph {
     // HBM message scratch for the workgroup kernels on graphs too large for LDS
     void* mws = nullptr;
     size_t mws_bytes = 0;
+    // QD_INPUT_PACKED decodes off the two-pass path: the inputs expanded to
+    // byte rows (grow only; DecodeArgs::unpack_buf)
+    void* ubuf = nullptr;
+    size_t ubuf_bytes = 0;
     size_t mws_failed = 0;  // smallest scratch size whose allocation failed (0: none)
     uint64_t mws_capped_calls = 0;  // calls served the reduced scratch since the failure
     // kernel timing ring (qd_graph_set_timing): 3 events per decode call
@@ -847,6 +851,22 @@ void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& 
     return G->mws;
 }
 
+// byte rows for a packed decode that does not take the two-pass path (every
+// input the call passes: syn [B][m], base and readout [B][n_data])
+void attach_unpack(qd_graph* G, DecodeArgs& a) {
+    if (!a.in_packed) return;
+    const size_t need = (size_t)a.B * ((size_t)G->dg.m + 2 * (size_t)G->dg.n_data) + 256;
+    if (need > G->ubuf_bytes) {
+        ws_drain(G);  // launches in flight may still read the old buffer
+        if (G->ubuf) hip_check(hipFree(G->ubuf), "hipFree unpack buffer");
+        G->ubuf = nullptr;
+        G->ubuf_bytes = 0;
+        hip_check(hipMalloc(&G->ubuf, need), "hipMalloc unpack buffer");
+        G->ubuf_bytes = need;
+    }
+    a.unpack_buf = static_cast<uint8_t*>(G->ubuf);
+}
+
 void note_kernels(qd_graph* G) {
     const LaunchNames& n = last_launch_names();
     G->last_bp = n.bp ? n.bp : "";
@@ -911,6 +931,9 @@ DecodeArgs make_args(const qd_graph* g, const qd_params* p, int64_t B, const uin
     a.ssf = p->ssf ? 1 : 0;
     a.ssf_max_steps = p->ssf_max_steps;
     a.syn_flags = p->syn_flags & 3;
+    a.in_packed = (p->syn_flags & QD_INPUT_PACKED) ? 1 : 0;
+    if (a.in_packed && (((uintptr_t)syn | (uintptr_t)base | (uintptr_t)readout) & 7))
+        throw Fail(-9, "QD_INPUT_PACKED rows must be 8-B aligned");
     a.ms_scaling = p->ms_scaling;
     a.syn = syn;
     a.base = base;
@@ -1193,6 +1216,7 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->ws) (void)hipFree(g->ws);
         if (g->qws) (void)hipFree(g->qws);
         if (g->mws) (void)hipFree(g->mws);
+        if (g->ubuf) (void)hipFree(g->ubuf);
         if (g->ctl) (void)hipFree(g->ctl);
         hgp_plan_destroy(g->hgp);
         free_timing(g);
@@ -1603,6 +1627,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         set_device(G);
         DecodeArgs a = make_args(G, p, B, syn, base, readout, x_out, corr_out, llr_out, iters, status, ssf_steps, fail);
         attach_queue(G, a, p->method, p->precision);
+        attach_unpack(G, a);
         attach_timing(G, a);
         size_t sb = 0;
         void* scr = message_scratch(G, p->method, p->precision, a, &sb);
@@ -1634,6 +1659,10 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         set_device(G);
         const DevGraph& g = G->dg;
         const size_t tsz = p->precision == QD_F32 ? 4 : 8;
+        // input row bytes: one byte per bit, or whole u64 words (QD_INPUT_PACKED)
+        const bool pk = (p->syn_flags & QD_INPUT_PACKED) != 0;
+        const size_t syn_row = pk ? ((size_t)g.m + 63) / 64 * 8 : (size_t)g.m;
+        const size_t dat_row = pk ? ((size_t)g.n_data + 63) / 64 * 8 : (size_t)g.n_data;
         // workspace layout (each region 256-B aligned)
         struct Reg { size_t off, bytes; };
         size_t off = 0;
@@ -1642,9 +1671,9 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
             if (on) off += (bytes + 255) / 256 * 256;
             return r;
         };
-        const Reg r_syn = reg((size_t)B * g.m, syn != nullptr);
-        const Reg r_base = reg((size_t)B * g.n_data, base != nullptr);
-        const Reg r_rd = reg((size_t)B * g.n_data, readout != nullptr);
+        const Reg r_syn = reg((size_t)B * syn_row, syn != nullptr);
+        const Reg r_base = reg((size_t)B * dat_row, base != nullptr);
+        const Reg r_rd = reg((size_t)B * dat_row, readout != nullptr);
         const Reg r_x = reg((size_t)B * g.n, x_out != nullptr);
         const Reg r_corr = reg((size_t)B * g.n_data, corr_out != nullptr);
         const Reg r_llr = reg((size_t)B * g.n * tsz, llr_out != nullptr);
@@ -1669,6 +1698,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
                                  (const uint8_t*)dptr(r_rd), (uint8_t*)dptr(r_x), (uint8_t*)dptr(r_corr), dptr(r_llr),
                                  (int32_t*)dptr(r_it), (uint8_t*)dptr(r_st), (int32_t*)dptr(r_ss), (uint8_t*)dptr(r_fl));
         attach_queue(G, a, p->method, p->precision);
+        attach_unpack(G, a);
         attach_timing(G, a);
         size_t sb = 0;
         void* scr = message_scratch(G, p->method, p->precision, a, &sb);
@@ -1692,14 +1722,15 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
     });
 }
 
-int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double p_meas, uint32_t seed,
-                             uint32_t stream_id, int64_t shot0, int64_t B, uint8_t* syn, uint8_t* readout,
-                             void* stream) {
+static int sample_storage(qd_graph* G, int32_t rounds, double p_data, double p_meas, uint32_t seed,
+                          uint32_t stream_id, int64_t shot0, int64_t B, uint8_t* syn, uint8_t* readout,
+                          void* stream, bool packed) {
     return guarded([&] {
         check_graph(G);
         if (rounds < 0 || B < 0) throw Fail(-60, "invalid sampler arguments");
         if (B == 0) return;
         if (!syn || !readout) throw Fail(-60, "invalid sampler arguments");
+        if (packed && (((uintptr_t)syn | (uintptr_t)readout) & 7)) throw Fail(-60, "packed rows must be 8-B aligned");
         if (G->dg.fold_blocks != 1 || G->dg.n_data != G->dg.n) throw Fail(-61, "sampler needs a plain code graph (H = Hz)");
         auto thr = [](double p) -> uint32_t {
             if (!(p > 0)) return 0u;
@@ -1708,9 +1739,22 @@ int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double 
         };
         set_device(G);
         const int rc = launch_sample_storage(G->dg, rounds, thr(2.0 * p_data / 3.0), thr(p_meas), seed, stream_id,
-                                             shot0, B, syn, readout, G->num_cus, (hipStream_t)stream);
+                                             shot0, B, syn, readout, G->num_cus, (hipStream_t)stream, packed);
         if (rc != 0) throw Fail(-102, std::string("sampler launch failed: ") + hipGetErrorString((hipError_t)rc));
     });
+}
+
+int qd_sample_storage_device(qd_graph* G, int32_t rounds, double p_data, double p_meas, uint32_t seed,
+                             uint32_t stream_id, int64_t shot0, int64_t B, uint8_t* syn, uint8_t* readout,
+                             void* stream) {
+    return sample_storage(G, rounds, p_data, p_meas, seed, stream_id, shot0, B, syn, readout, stream, false);
+}
+
+int qd_sample_storage_packed_device(qd_graph* G, int32_t rounds, double p_data, double p_meas, uint32_t seed,
+                                    uint32_t stream_id, int64_t shot0, int64_t B, uint64_t* syn, uint64_t* readout,
+                                    void* stream) {
+    return sample_storage(G, rounds, p_data, p_meas, seed, stream_id, shot0, B, reinterpret_cast<uint8_t*>(syn),
+                          reinterpret_cast<uint8_t*>(readout), stream, true);
 }
 
 int qd_osd_device_supported(const qd_graph* G) {

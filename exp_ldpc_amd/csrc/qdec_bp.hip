@@ -979,9 +979,11 @@ static bool lean_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
 // min-sum launches whose graph has the slot-order logicals (or no fused check);
 // QDEC_COMPACT=0 keeps the one-pass kernel (A/B, parity tests run both).
 static bool compact_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
-    // the triage reads 16-B chunks: 16-B aligned syndrome / readout buffers only;
+    // the triage reads 16-B chunks of byte rows (16-B aligned syndrome / readout
+    // buffers only) or u64 words of packed rows (8-B aligned, checked by the ABI);
     // its list counters take u64 atomics (natural alignment), entries 16-B stores
-    if ((reinterpret_cast<uintptr_t>(a.syn) & 15) || (a.readout && (reinterpret_cast<uintptr_t>(a.readout) & 15)))
+    const uintptr_t al = a.in_packed ? 7 : 15;
+    if ((reinterpret_cast<uintptr_t>(a.syn) & al) || (a.readout && (reinterpret_cast<uintptr_t>(a.readout) & al)))
         return false;
     if ((reinterpret_cast<uintptr_t>(a.cmp_count) & 127) || (reinterpret_cast<uintptr_t>(a.cmp) & 15)) return false;
     const bool want_fail = a.fail && a.readout && g.k > 0;
@@ -991,14 +993,16 @@ static bool compact_launch(const DevGraph& g, const DecodeArgs& a, bool defer) {
 template <int RC, int RV>
 static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t stream) {
     const bool want_fail = a.fail && a.readout && g.k > 0;
-    // the tile loads are 16-B vector loads
-    if ((reinterpret_cast<uintptr_t>(a.syn) & 15) || (want_fail && (reinterpret_cast<uintptr_t>(a.readout) & 15)))
+    // the tile loads are 16-B vector loads (packed rows: u64 loads)
+    const uintptr_t al = a.in_packed ? 7 : 15;
+    if ((reinterpret_cast<uintptr_t>(a.syn) & al) || (want_fail && (reinterpret_cast<uintptr_t>(a.readout) & al)))
         return (int)hipErrorInvalidValue;
     if (a.it1_lut && (!g.it1_vchk || !g.it1_cvar || g.m_pad != 64 * RC || g.n_pad != 64 * RV))
         return (int)hipErrorInvalidValue;
     // the logicals, the tile images, the iteration-1 words (byte images: over
     // the images; the kernel's layout, ms_triage_kernel)
-    const size_t tiles = triage_img_bytes(64 * (int64_t)g.m) + triage_img_bytes(64 * (int64_t)g.n_data);
+    const size_t tiles =
+        a.in_packed ? 0 : triage_img_bytes(64 * (int64_t)g.m) + triage_img_bytes(64 * (int64_t)g.n_data);
     const size_t it1 = a.it1_lut ? TriageIt1<RC, RV>::bytes : 0;
     const size_t lds = ((want_fail ? (size_t)g.k * g.lz_words * 8 : 0) + 15) / 16 * 16 +
                        tiles + it1;
@@ -1174,10 +1178,76 @@ bool wave_kernel_supports(const DevGraph& g) {
     return shape && g.max_rdeg <= kDR && g.max_cdeg <= kDC && g.k <= 256;
 }
 
-int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a, int num_cus,
+// ---------------------------------------------------------------- packed inputs
+// Bit-packed rows (QD_INPUT_PACKED) expanded to one byte per bit: dst[r][c] =
+// bit c of src row r (words of `words` u64 per row).  Grid-stride over 4-byte
+// groups of the output (coalesced stores; the source words are re-read from
+// L1/L2 by neighbouring threads).
+__global__ void unpack_rows_kernel(const uint64_t* __restrict__ src, int64_t rows, int cols, int words,
+                                   uint8_t* __restrict__ dst) {
+    const int64_t total = rows * cols;
+    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; e < total;
+         e += (int64_t)gridDim.x * blockDim.x * 4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t q = e + t;
+            if (q < total) {
+                const int64_t r = q / cols;
+                const int c = (int)(q - r * cols);
+                dst[q] = (uint8_t)((src[r * words + (c >> 6)] >> (c & 63)) & 1ull);
+            }
+        }
+    }
+}
+
+static int launch_unpack_rows(const uint8_t* src, int64_t rows, int cols, uint8_t* dst, int num_cus,
+                              hipStream_t stream) {
+    if (rows <= 0 || cols <= 0) return 0;
+    const int64_t groups = (rows * cols + 3) / 4;
+    const long long blocks = std::min<long long>((groups + 255) / 256, (long long)num_cus * 16);
+    hipLaunchKernelGGL(unpack_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const uint64_t*>(src), rows, cols, (cols + 63) / 64, dst);
+    return (int)hipGetLastError();
+}
+
+// A packed decode the triage can read directly: a lean min-sum launch on a wave
+// graph that takes the two-pass path (launch_wave / launch_bp_wave's choice).
+static bool packed_two_pass(const DevGraph& g, int method, const DecodeArgs& a0) {
+    if (method != 1 || !g.wave || !wave_kernel_supports(g)) return false;
+    DecodeArgs a = a0;
+    const bool ssf_wave = g.n_gen <= 128 && g.g_lc8;
+    a.q_packed = a.ssf && ssf_wave ? 1 : 0;
+    if (a.ssf) return ssf_wave && g.k <= g.n_pad && compact_launch(g, a, true);
+    return compact_launch(g, a, false);
+}
+
+int launch_decode(const DevGraph& g, int method, int precision, const DecodeArgs& a0, int num_cus,
                   hipStream_t stream, void* scratch, size_t scratch_bytes) {
     last_launch_names() = LaunchNames{};
-    if (a.B <= 0) return 0;
+    if (a0.B <= 0) return 0;
+    DecodeArgs a = a0;
+    if (a.in_packed && !packed_two_pass(g, method, a)) {
+        // every other path reads byte rows: expand the inputs first
+        if (!a.unpack_buf) return (int)hipErrorInvalidValue;
+        uint8_t* u = a.unpack_buf;
+        int rc = 0;
+        if (a.syn) {
+            rc = launch_unpack_rows(a.syn, a.B, g.m, u, num_cus, stream);
+            a.syn = u;
+            u += (size_t)a.B * g.m;
+        }
+        if (rc == 0 && a.base) {
+            rc = launch_unpack_rows(a.base, a.B, g.n_data, u, num_cus, stream);
+            a.base = u;
+            u += (size_t)a.B * g.n_data;
+        }
+        if (rc == 0 && a.readout) {
+            rc = launch_unpack_rows(a.readout, a.B, g.n_data, u, num_cus, stream);
+            a.readout = u;
+        }
+        if (rc != 0) return rc;
+        a.in_packed = 0;
+    }
     if (!g.wave || !wave_kernel_supports(g))
         return launch_decode_block(g, method, precision, a, num_cus, stream, scratch, scratch_bytes);
     if (precision == 1)

@@ -876,10 +876,11 @@ __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs
     // row_bits reads one dword past a row)
     uint64_t* lz_lds = reinterpret_cast<uint64_t*>(smem);
     const int nlz = want_fail ? g.k * g.lz_words : 0;
+    const bool pk = a.in_packed != 0;  // bit-packed input rows: no tile images
     unsigned char* syn_img = smem + ((size_t)nlz * 8 + 15) / 16 * 16;
-    unsigned char* rd_img = syn_img + triage_img_bytes(64 * (int64_t)m);
+    unsigned char* rd_img = syn_img + (pk ? 0 : triage_img_bytes(64 * (int64_t)m));
     // iteration-1 words: past the images
-    unsigned char* it1_base = rd_img + triage_img_bytes(64 * (int64_t)nd);
+    unsigned char* it1_base = rd_img + (pk ? 0 : triage_img_bytes(64 * (int64_t)nd));
     for (int e = lane; e < nlz; e += 64) lz_lds[e] = g.lz[e];
     // iteration-1 tables (TriageIt1), loaded ahead of the tiles
     uint64_t it_ids[NWD], it_cv[RC][2];
@@ -896,22 +897,44 @@ __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs
             it_cv[rc][1] = g.it1_cvar[2 * (rc * 64 + lane) + 1];
         }
     }
-    const TileSrc ts(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img);
-    const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
-                     want_fail ? (int64_t)ns * nd : 0, rd_img);
-    if (want_fail)
-        tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < kTriageUB ? 4 * NWD : kTriageUB)>(ts, tr, lane);
-    else tile_to_lds<8>(ts, lane);
-    __syncthreads();
-    const int ssh = ts.shift, rsh = tr.shift;
     const bool live = lane < ns;
     const int64_t shot = s0 + lane;
     uint64_t sw[RC];
-    row_bits_b<RC>(reinterpret_cast<const uint32_t*>(syn_img), ssh + lane * m, m, sw);
+    uint64_t rw[NWD];
+    if (pk) {
+        // one row of u64 words per shot (RC = ceil(m / 64), NWD = ceil(n_data / 64)
+        // on wave graphs): lane-strided loads, padding bits cleared
+        const uint64_t* sp = reinterpret_cast<const uint64_t*>(a.syn) + min(shot, a.B - 1) * RC;
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) {
+            uint64_t v = __builtin_nontemporal_load(sp + rc);
+            if (64 * rc + 64 > m) v &= (m - 64 * rc >= 64) ? ~0ull : ((1ull << (m - 64 * rc)) - 1ull);
+            sw[rc] = live ? v : 0ull;
+        }
+        if (want_fail) {
+            const int rdw = (nd + 63) / 64;
+            const uint64_t* rq = reinterpret_cast<const uint64_t*>(a.readout) + min(shot, a.B - 1) * rdw;
+#pragma unroll
+            for (int w = 0; w < NWD; ++w) {
+                uint64_t v = w < rdw ? __builtin_nontemporal_load(rq + w) : 0ull;
+                if (64 * w + 64 > nd) v &= (nd - 64 * w >= 64) ? ~0ull : (nd > 64 * w ? (1ull << (nd - 64 * w)) - 1ull : 0ull);
+                rw[w] = v;
+            }
+        }
+        __syncthreads();  // the logicals' LDS copy (above) before its reads
+    } else {
+        const TileSrc ts(a.syn, a.B * (int64_t)m, s0 * m, (int64_t)ns * m, syn_img);
+        const TileSrc tr(want_fail ? a.readout : a.syn, want_fail ? a.B * (int64_t)nd : 0, s0 * nd,
+                         want_fail ? (int64_t)ns * nd : 0, rd_img);
+        if (want_fail)
+            tile_pair_to_lds<(4 * RC < 8 ? 4 * RC : 8), (4 * NWD < kTriageUB ? 4 * NWD : kTriageUB)>(ts, tr, lane);
+        else tile_to_lds<8>(ts, lane);
+        __syncthreads();
+        row_bits_b<RC>(reinterpret_cast<const uint32_t*>(syn_img), ts.shift + lane * m, m, sw);
+        if (want_fail) row_bits_b<NWD>(reinterpret_cast<const uint32_t*>(rd_img), tr.shift + lane * nd, nd, rw);
+    }
     uint64_t rp[kMaxLogicalRounds] = {0ull, 0ull, 0ull, 0ull};
     if (want_fail) {
-        uint64_t rw[NWD];
-        row_bits_b<NWD>(reinterpret_cast<const uint32_t*>(rd_img), rsh + lane * nd, nd, rw);
         for (int r = 0; r < g.k; ++r) {  // uniform rows of the dense logical table (LDS broadcasts)
             int par = 0;
 #pragma unroll

@@ -247,6 +247,13 @@ struct DecodeArgs {
     // packed SSF queue entries carry the readout's logical parities (bit r of
     // the dw area = parity of Lz[r] . readout) instead of the readout words
     int q_rpar;
+    // QD_INPUT_PACKED: syn / base / readout are bit-packed rows of u64 words
+    // (syn [B][ceil(m/64)], base / readout [B][ceil(n_data/64)]; bit j of word
+    // w = element 64 w + j).  The two-pass path's triage reads them directly;
+    // every other path first expands them into unpack_buf (library-owned,
+    // B * (m + 2 n_data) bytes) with unpack_rows_kernel.
+    int in_packed;
+    uint8_t* unpack_buf;
 };
 
 // Arguments of the GPU OSD stage (qdec_osd.hip).  Shots whose status has bit 0
@@ -328,7 +335,7 @@ bool group_kernel_applies(const DevGraph& g, int method, int precision, const De
 bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a);
 int launch_sample_storage(const DevGraph& g, int rounds, uint32_t thr_data, uint32_t thr_meas,
                           uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
-                          uint8_t* syn, uint8_t* readout, int num_cus, hipStream_t stream);
+                          uint8_t* syn, uint8_t* readout, int num_cus, hipStream_t stream, bool packed = false);
 int launch_count_flags(const uint8_t* flags, int64_t B, uint8_t mask, int64_t* out, hipStream_t stream);
 
 // ---------------------------------------------------------------- HGP kernel

@@ -157,14 +157,20 @@ class Decoder:
 
     # ------------------------------------------------------------ decoding
     def decode(self, syn=None, *, base=None, readout=None, syn_flags: int = 0, ssf: bool | None = None,
-               want=("x", "corr", "iters", "status", "ssf_steps", "fail")) -> dict:
+               want=("x", "corr", "iters", "status", "ssf_steps", "fail"), packed: bool = False) -> dict:
         """Decode B shots from host arrays; returns numpy arrays for `want`
-        (any of x, corr, llr, iters, status, ssf_steps, fail)."""
+        (any of x, corr, llr, iters, status, ssf_steps, fail).  packed=True:
+        syn / base / readout are bit-packed rows (uint64 words, pack_rows;
+        QD_INPUT_PACKED)."""
         def u8(a, cols):
             if a is None:
                 return None
+            if packed:
+                return np.ascontiguousarray(np.asarray(a), dtype=np.uint64).reshape(-1, (cols + 63) // 64)
             a = np.ascontiguousarray(np.asarray(a), dtype=np.uint8)
             return a.reshape(-1, cols)
+        if packed:
+            syn_flags = int(syn_flags) | QD_INPUT_PACKED
         syn = u8(syn, self.m)
         base = u8(base, self.n_data)
         readout = u8(readout, self.n_data)
@@ -197,15 +203,22 @@ class Decoder:
 
     def decode_device(self, B: int, *, syn=None, base=None, readout=None, x=None, corr=None, llr=None,
                       iters=None, status=None, ssf_steps=None, fail=None, syn_flags: int = 0,
-                      ssf: bool | None = None, stream=None) -> None:
+                      ssf: bool | None = None, stream=None, packed: bool = False) -> None:
         """Enqueue a decode of B device-resident shots (torch tensors or raw
-        device pointers) on `stream` (default: torch's current stream)."""
+        device pointers) on `stream` (default: torch's current stream).
+        packed=True: syn / base / readout are bit-packed rows, int64 tensors
+        [B][ceil(m/64)] / [B][ceil(n_data/64)] (sample_storage_device(packed=True)
+        writes them; QD_INPUT_PACKED)."""
         if stream is None:
             stream = _current_stream(self.device)
         B = int(B)
         llr_t = "float32" if self.precision == _abi.QD_F32 else "float64"
-        for name, t, dt, cols in (("syn", syn, "uint8", self.m), ("base", base, "uint8", self.n_data),
-                                  ("readout", readout, "uint8", self.n_data), ("x", x, "uint8", self.n),
+        in_t = "int64" if packed else "uint8"
+        wcols = (lambda c: (c + 63) // 64) if packed else (lambda c: c)
+        if packed:
+            syn_flags = int(syn_flags) | QD_INPUT_PACKED
+        for name, t, dt, cols in (("syn", syn, in_t, wcols(self.m)), ("base", base, in_t, wcols(self.n_data)),
+                                  ("readout", readout, in_t, wcols(self.n_data)), ("x", x, "uint8", self.n),
                                   ("corr", corr, "uint8", self.n_data), ("llr", llr, llr_t, self.n),
                                   ("iters", iters, "int32", 1), ("status", status, "uint8", 1),
                                   ("ssf_steps", ssf_steps, "int32", 1), ("fail", fail, "uint8", 1)):
@@ -232,10 +245,20 @@ class Decoder:
             raise ValueError(f"{name}: {t.numel()} elements, the batch needs {numel}")
 
     def sample_storage_device(self, rounds: int, p_data: float, p_meas: float, seed: int, stream_id: int,
-                              shot0: int, B: int, syn, readout, stream=None) -> None:
-        """Storage-experiment sampler (H must be the plain Hz graph)."""
+                              shot0: int, B: int, syn, readout, stream=None, packed: bool = False) -> None:
+        """Storage-experiment sampler (H must be the plain Hz graph).  packed=True
+        writes bit-packed rows: syn int64 [B][ceil((rounds+1) m / 64)], readout
+        int64 [B][ceil(n / 64)] (the same shots as the byte rows, pack_rows of them)."""
         if stream is None:
             stream = _current_stream(self.device)
+        if packed:
+            self._check_device_buffer("syn", syn, "int64", B * (((rounds + 1) * self.m + 63) // 64))
+            self._check_device_buffer("readout", readout, "int64", B * ((self.n + 63) // 64))
+            _abi.check(self._lib.qd_sample_storage_packed_device(
+                self._handle, int(rounds), float(p_data), float(p_meas), int(seed) & 0xFFFFFFFF,
+                int(stream_id) & 0xFFFFFFFF, int(shot0), int(B), _abi.ptr(syn), _abi.ptr(readout),
+                C.c_void_p(stream)), "qd_sample_storage_packed_device")
+            return
         _abi.check(self._lib.qd_sample_storage_device(
             self._handle, int(rounds), float(p_data), float(p_meas), int(seed) & 0xFFFFFFFF,
             int(stream_id) & 0xFFFFFFFF, int(shot0), int(B), _abi.ptr(syn), _abi.ptr(readout), C.c_void_p(stream)),
@@ -350,6 +373,31 @@ class Decoder:
             self.close()
         except Exception:
             pass
+
+
+QD_INPUT_PACKED = _abi.QD_INPUT_PACKED  # qd_syn_flags: bit-packed input rows
+
+
+def pack_rows(bits) -> np.ndarray:
+    """Bit-pack 0/1 rows (uint8 [B][L]) into the QD_INPUT_PACKED layout: uint64
+    [B][ceil(L/64)], bit j of word w = element 64 w + j (little-endian: byte for
+    byte Stim's bit_packed=True rows, zero-padded to 8 bytes)."""
+    a = np.asarray(bits, dtype=np.uint8) & 1
+    a = a.reshape(a.shape[0], -1) if a.ndim > 1 else a.reshape(1, -1)
+    B, L = a.shape
+    W = (L + 63) // 64
+    by = np.packbits(a, axis=1, bitorder="little")
+    out = np.zeros((B, W * 8), np.uint8)
+    out[:, :by.shape[1]] = by
+    return out.view("<u8").reshape(B, W).astype(np.uint64)
+
+
+def unpack_rows(words, length: int) -> np.ndarray:
+    """Inverse of pack_rows: uint8 [B][length]."""
+    w = np.ascontiguousarray(np.asarray(words).astype("<u8"))
+    B = w.shape[0] if w.ndim > 1 else 1
+    by = w.reshape(B, -1).view(np.uint8)
+    return np.unpackbits(by, axis=1, bitorder="little")[:, :length].astype(np.uint8)
 
 
 def count_flags_device(flags, B: int, mask: int, out, stream=None, device: int = 0) -> None:

@@ -40,7 +40,14 @@ typedef struct qd_graph qd_graph;
 
 enum qd_method { QD_PRODUCT_SUM = 0, QD_MIN_SUM = 1 };      /* ldpc bp_method 'ps' / 'ms','msl' */
 enum qd_precision { QD_F64 = 0, QD_F32 = 1 };               /* message arithmetic */
-enum qd_syn_flags { QD_SYN_ADD_BASE = 1, QD_SYN_ADD_READOUT = 2 };
+/* syn_flags bits.  QD_INPUT_PACKED: the decode's syn / base / readout inputs are
+ * bit-packed rows of little-endian u64 words instead of one byte per bit:
+ * syn [B][ceil(m/64)], base / readout [B][ceil(n_data/64)], bit j of word w =
+ * element 64 w + j, padding bits ignored, 8-B aligned.  Byte for byte this is
+ * Stim's sample(bit_packed=True) layout (the reference sampler,
+ * _experiment.py:196-197) with each row zero-padded to a multiple of 8 bytes.
+ * Outputs keep their layouts. */
+enum qd_syn_flags { QD_SYN_ADD_BASE = 1, QD_SYN_ADD_READOUT = 2, QD_INPUT_PACKED = 16 };
 enum qd_status_bits { QD_ST_BP_CONVERGED = 1, QD_ST_SATISFIED = 2 };
 
 typedef struct qd_params {
@@ -142,6 +149,13 @@ int qd_decode_batch_device(qd_graph* g, const qd_params* prm, int64_t B,
 int qd_sample_storage_device(qd_graph* g, int32_t rounds, double p_data, double p_meas,
                              uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
                              uint8_t* syn, uint8_t* readout, void* stream);
+/* The same shots, written bit-packed (the QD_INPUT_PACKED layout):
+ *   syn     uint64 [B][ceil((rounds+1)*m/64)]   readout uint64 [B][ceil(n/64)]
+ * 8-B aligned buffers.  With rounds = 0 the rows feed qd_decode_batch_device
+ * with QD_INPUT_PACKED directly (42 B per shot at n = 225 instead of 333). */
+int qd_sample_storage_packed_device(qd_graph* g, int32_t rounds, double p_data, double p_meas,
+                                    uint32_t seed, uint32_t stream_id, int64_t shot0, int64_t B,
+                                    uint64_t* syn, uint64_t* readout, void* stream);
 
 /* Ordered-statistics decoding of shots BP did not converge on (the OSD stage of
  * ldpc v1 bposd_decoder; reference _experiment.py:23-27, 37-40, 77, 96-100).  Host

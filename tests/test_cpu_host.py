@@ -611,3 +611,22 @@ def test_hgp_kernel_plan_and_rtc_compile(code225):
     h3, _, _ = _host_graph(lib, P, probs=0.01)
     assert lib.qd_graph_hgp_info(h3, info) == 0
     lib.qd_graph_destroy(h3)
+
+
+def test_pack_rows_layout():
+    """pack_rows (QD_INPUT_PACKED): bit j of u64 word w = element 64 w + j,
+    little-endian bytes, so its bytes equal np.packbits(bitorder='little') of the
+    row (Stim's bit_packed rows) zero-padded to 8 bytes; unpack_rows inverts it."""
+    from exp_ldpc_amd.decoder import pack_rows, unpack_rows
+    rng = np.random.default_rng(4)
+    for L in (1, 63, 64, 65, 108, 225, 1000):
+        a = rng.integers(0, 2, (5, L)).astype(np.uint8)
+        w = pack_rows(a)
+        assert w.dtype == np.uint64 and w.shape == (5, (L + 63) // 64)
+        for b in range(5):
+            for j in range(L):
+                assert (int(w[b, j // 64]) >> (j % 64)) & 1 == a[b, j]
+        by = w.view(np.uint8)
+        pb = np.packbits(a, axis=1, bitorder="little")
+        assert np.array_equal(by[:, :pb.shape[1]], pb) and not by[:, pb.shape[1]:].any()
+        assert np.array_equal(unpack_rows(w, L), a)
