@@ -885,6 +885,8 @@ def main():
                          "and roofline, every config line; the stdout line names it")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 line (c3_line; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--ssf-fuse", type=int, default=1, choices=[0, 1],
+                    help="1: SSF inside the compact BP kernel (QD_OPT_SSF_FUSE); 0: queue + ssf_lut_kernel")
     # diagnostic: decode without SSF (prices SSF inside the overlapped step)
     ap.add_argument("--no-ssf-exp", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -922,8 +924,11 @@ def main():
             return [FakeDecoder(dev) for _ in ps]
         from exp_ldpc_amd.decoder import Decoder
         # one decoder graph per sweep point (priors differ), sharing nothing mutable
-        return [Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0,
-                        flip_sets=hx, logicals=lz, device=local) for p in ps]
+        ds = [Decoder(hz, 2 * p / 3, method="ms", precision=precision, max_iter=50, ms_scaling=0.0,
+                      flip_sets=hx, logicals=lz, device=local) for p in ps]
+        for d in ds:
+            d.set_option("ssf_fuse", args.ssf_fuse)
+        return ds
 
     run = Run(args, ps, m, n, world, rank, dev, torch, fake)
     decs = decoders(args.precision)

@@ -1923,6 +1923,7 @@ int qd_graph_set_option(qd_graph* G, int32_t option, int32_t value) {
             case QD_OPT_SSF_INC: in(0, 1); g.opt_ssf_inc = value; break;
             case QD_OPT_BLOCK_WG: in(0, 64); g.opt_block_wg = value; break;
             case QD_OPT_GROUP_MB: in(0, 1 << 22); g.opt_group_mb = value; break;
+            case QD_OPT_SSF_FUSE: in(0, 1); g.opt_ssf_fuse = value; break;
             default: throw Fail(-2, "unknown option");
         }
     });
@@ -1942,6 +1943,7 @@ int qd_graph_get_option(const qd_graph* G, int32_t option, int32_t* value) {
             case QD_OPT_SSF_INC: *value = g.opt_ssf_inc; break;
             case QD_OPT_BLOCK_WG: *value = g.opt_block_wg; break;
             case QD_OPT_GROUP_MB: *value = g.opt_group_mb; break;
+            case QD_OPT_SSF_FUSE: *value = g.opt_ssf_fuse; break;
             default: throw Fail(-2, "unknown option");
         }
     });

@@ -1016,7 +1016,7 @@ static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t str
     return (int)hipGetLastError();
 }
 
-template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER>
+template <typename T, int METHOD, int RC, int RV, int DRC, bool DEFER, int FUSE = 0>
 static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if constexpr (METHOD == 1) {
         // the fused failure check reads the dense logical table's LDS copy
@@ -1048,6 +1048,7 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             if (b.ev) (void)hipEventRecord(b.ev[3], stream);  // end of the pre-pass
             size_t clds = MsLds<T>::core_bytes(g) + ((size_t)g.k * RV * 8 + 15) / 16 * 16 +
                           2 * kCmpLists * kCmpSegs * 8;
+            if (FUSE) clds += ((size_t)RV * 8 + (size_t)g.m_pad * 2 + 15) / 16 * 16;  // fused SSF: xb, flog
             // a capped grid (f64: 8 waves per CU) must also be placed evenly: the
             // dispatcher stacks up to the kernel's own occupancy on a CU (11 for
             // the 159-VGPR f64 kernel) while others sit idle, so the LDS request is
@@ -1058,19 +1059,19 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
                 if (g.ms_d3r >= 2) {
                     if constexpr (sizeof(T) == 8) {
                         if (cap > 8) {  // 3 waves per SIMD
-                            QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 2, 3);
-                            return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 2, 3>, clds, b.B,
+                            QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 2, 3, FUSE);
+                            return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 2, 3, FUSE>, clds, b.B,
                                                      num_cus, stream, g, b, 64, cap);
                         }
                     }
-                    QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 2, 0);
-                    return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 2>, clds, b.B, num_cus, stream,
-                                             g, b, 64, cap);
+                    QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 2, 0, FUSE);
+                    return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 2, 0, FUSE>, clds, b.B, num_cus,
+                                             stream, g, b, 64, cap);
                 }
             }
-            QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 0, 0);
-            return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 0>, clds, b.B, num_cus, stream, g, b, 64,
-                                     cap);
+            QDEC_NOTE_BP("qdec::bp_ms_cmp_kernel", tname<T>(), RC, RV, DRC, DEFER, 0, 0, FUSE);
+            return launch_persistent(bp_ms_cmp_kernel<T, RC, RV, DRC, DEFER, 0, 0, FUSE>, clds, b.B, num_cus, stream,
+                                     g, b, 64, cap);
         }
         // degree-3 rounds: the (2, 4, 7) shape (n = 225 HGP: 144 degree-3 columns) instantiates D3R = 2
         if constexpr (RC == 2 && RV == 4 && DRC == 7) {
@@ -1125,6 +1126,18 @@ static int launch_wave(const DevGraph& g, const DecodeArgs& a0, int num_cus, hip
         return rc;
     }
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
+    if constexpr (METHOD == 1) {
+        // fused SSF: the compact BP kernel runs the table-driven SSF itself
+        // (QD_OPT_SSF_FUSE; same tables and spec as ssf_lut_kernel)
+        if (a.q_rpar && g.opt_ssf_fuse && g.s_lut && g.s_tog && g.opt_ssf == kSsfAuto && g.n_gen <= 128) {
+            record_ev(a, 0, stream);
+            const int rc = g.n_gen <= 64 ? launch_bp_wave<T, METHOD, RC, RV, DRC, true, 1>(g, a, num_cus, stream)
+                                         : launch_bp_wave<T, METHOD, RC, RV, DRC, true, 2>(g, a, num_cus, stream);
+            record_ev(a, 1, stream);
+            record_ev(a, 2, stream);
+            return rc;
+        }
+    }
     if (!a.q_rpar) {  // the compact path's triage zeroes both counters itself (one launch fewer each)
         hipError_t e = hipMemsetAsync(a.q_count, 0, sizeof(int32_t), stream);
         if (e == hipSuccess && a.wave_ctr)  // the SSF kernel's slot counter (ShotSeq)

@@ -1072,12 +1072,117 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Small-set-flip of one BP-failed shot inside the compact BP kernel (FUSE > 0,
+// QD_OPT_SSF_FUSE): the table-driven spec of ssf_lut_kernel (qdec_bp.hip), with
+// the same tables (s_lut, s_off, s_lcw, s_tog), the same key, the same step
+// order and the same flip application, so the same outputs; the tables are read
+// through the cache hierarchy instead of a workgroup's LDS copy, and the shot
+// never goes through the HBM queue or a second launch.  RG: generators per lane
+// (n_gen <= 64 * RG).  xb: the wave's hard decision by column as LDS bit words
+// (updated in place); flog: the wave's step log; R: residual words by check.
+// Returns the steps taken; sw_out = the residual weight left.
+template <int RG, int RW>
+__device__ __forceinline__ int ssf_fused(const DevGraph& g, int max_steps, uint32_t* xb, uint16_t* flog,
+                                      const uint64_t* Rin, int lane, int* sw_out) {
+    const uint32_t* __restrict__ lut = g.s_lut;
+    const uint32_t* __restrict__ tog = g.s_tog;
+    // this lane's generators' table offsets (the winner's local-check ids are read
+    // per step at a wave-uniform address instead of being held in registers)
+    uint32_t off[RG];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) off[rg] = g.s_off[rg * 64 + lane];
+    // first local syndromes: the toggle rows of the violated checks, 8 rows per
+    // round (independent loads; row m_pad is all zero)
+    const uint32_t zrow = (uint32_t)g.m_pad;
+    uint32_t sl = 0;
+    int sw = 0;
+#pragma unroll
+    for (int w = 0; w < RW; ++w) {
+        uint64_t bits = Rin[w];
+        sw += __popcll(bits);
+        while (bits) {
+            uint32_t t = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                uint32_t c = zrow;
+                if (bits) {
+                    c = (uint32_t)(w * 64 + __builtin_ctzll(bits));
+                    bits &= bits - 1;
+                }
+                t ^= tog[c * 64 + lane];
+            }
+            sl ^= t;
+        }
+    }
+    int steps = 0;
+    while (sw > 0 && (max_steps <= 0 || steps < max_steps)) {
+        // every generator's best (rank, -g, t); wave max
+        uint32_t e[RG];
+        int kv = 0;
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+            const uint32_t s = rg ? (sl >> 16) : (sl & 0xffffu);
+            e[rg] = lut[off[rg] + s];
+            const uint32_t rank = e[rg] >> 24;
+            const int key = rank ? (int)((rank << 15) | ((uint32_t)(127 - (rg * 64 + lane)) << 8) | (e[rg] & 0xffu)) : 0;
+            kv = max(kv, key);
+        }
+        const int best = wave_max_i32(kv);
+        if (best == 0) break;  // no positive gain left
+        const int gsel = 127 - ((best >> 8) & 127);
+        const int tsel = best & 255;
+        const int owner = gsel & 63;
+        const bool hi = RG == 2 && gsel >= 64;
+        const uint32_t esel = (uint32_t)__builtin_amdgcn_readlane((int)(hi ? e[RG - 1] : e[0]), owner);
+        const uint32_t slg = ((uint32_t)__builtin_amdgcn_readlane((int)sl, owner) >> (hi ? 16 : 0)) & 0xffffu;
+        const uint32_t fm = (esel >> 8) & 0xffffu;
+        sw -= __builtin_popcount(slg) - __builtin_popcount(slg ^ fm);
+        ++steps;
+        // toggle the flipped checks' local-syndrome bits (all loads issued first)
+        uint32_t tr[kLutLC];
+#pragma unroll
+        for (int w = 0; w < kLutLCW; ++w) {
+            const uint32_t nib = (fm >> (4 * w)) & 0xfu;
+            const uint32_t word = nib ? g.s_lcw[w * g.g_pad + gsel] : 0u;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                tr[4 * w + b] = 0u;
+                if ((nib >> b) & 1u) tr[4 * w + b] = tog[((word >> (8 * b)) & 0xffu) * 64 + lane];
+            }
+        }
+        uint32_t tg = 0;
+#pragma unroll
+        for (int b = 0; b < kLutLC; ++b) tg ^= tr[b];
+        sl ^= tg;
+        if (lane == 0) flog[steps - 1] = (uint16_t)(gsel | (tsel << 8));
+    }
+    wave_lds_sync();
+    // x ^= 1_F of every logged step (a qubit flipped twice cancels, in any order)
+    for (int b0 = 0; b0 < steps; b0 += 64) {
+        if (b0 + lane < steps) {
+            const uint32_t e = flog[b0 + lane];
+            const int gg = (int)(e & 0xffu);
+#pragma unroll
+            for (int k = 0; k < kGenW; ++k)
+                if ((e >> (8 + k)) & 1u) {
+                    const uint32_t q = g.g_q[k * g.g_pad + gg];
+                    atomicXor(&xb[q >> 5], 1u << (q & 31));
+                }
+        }
+    }
+    wave_lds_sync();
+    *sw_out = sw;
+    return steps;
+}
+
 // The compact-list BP kernel (see above): the lean bp_ms_wave_kernel's BP
 // (MsCore) on the listed shots only.  Entries come in chunks of up to
 // CmpEntry::kPer (one u64 per lane, the next chunk loaded while this one
 // decodes; a list shorter than kPer entries per wave is cut finer); chunks are
 // handed out by ShotSeq (static stride, then a counter for the tail).
-template <typename T, int RC, int RV, int DRC, bool DEFER, int D3R, int OCC = 0>
+// FUSE (with DEFER): 0 = BP-failed shots go to the SSF queue; 1 / 2 = SSF runs
+// here (ssf_fused with RG = FUSE generators per lane).
+template <typename T, int RC, int RV, int DRC, bool DEFER, int D3R, int OCC = 0, int FUSE = 0>
 __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void bp_ms_cmp_kernel(DevGraph g, DecodeArgs a) {
     using Core = MsCore<T, RC, RV, DRC, true, D3R>;
     using Ent = CmpEntry<RC>;
@@ -1186,7 +1291,48 @@ __global__ __launch_bounds__(64, OCC > 0 ? OCC : (sizeof(T) == 4 ? 4 : 2)) void 
             QDEC_COUNT(8, iters);
             QDEC_COUNT(9, 1);
             if (lane == 0 && a.iters) a.iters[shot] = iters;
-            if (DEFER && !conv) {
+            if (DEFER && FUSE && !conv) {
+                // SSF right here: hard decision by column as LDS bit words, residual
+                // by check, then the table-driven flips (ssf_fused)
+                uint64_t* xb = reinterpret_cast<uint64_t*>(seg_cnt + 2 * kCmpSegs);  // [RV] (kernel LDS tail)
+                uint16_t* flog = reinterpret_cast<uint16_t*>(xb + RV);                // [m_pad]
+#pragma unroll
+                for (int rv = 0; rv < RV; ++rv) xh[core.col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);
+                wave_lds_sync();
+                uint64_t rw[RC];
+#pragma unroll
+                for (int w = 0; w < RV; ++w) {
+                    const uint64_t xw = __ballot(xh[w * 64 + lane] & 1);
+                    if (lane == 0) xb[w] = xw;
+                }
+#pragma unroll
+                for (int rc = 0; rc < RC; ++rc) rw[rc] = __ballot(pres[rc]);
+                wave_lds_sync();
+                int sw = 0;
+                const int steps = ssf_fused<(FUSE > 0 ? FUSE : 1), RC>(g, a.ssf_max_steps,
+                                                                       reinterpret_cast<uint32_t*>(xb), flog, rw,
+                                                                       lane, &sw);
+                int f = 0;
+                if (want_fail) {  // Lz (by column, the graph's dense table) x against the readout parities
+#pragma unroll
+                    for (int rr = 0; rr < kMaxLogicalRounds; ++rr) {
+                        const int r = rr * 64 + lane;
+                        if (r < g.k) {
+                            int par = (int)((rpar[rr] >> lane) & 1);
+                            for (int w = 0; w < g.lz_words && w < RV; ++w)
+                                par += __popcll(g.lz[(size_t)r * g.lz_words + w] & xb[w]);
+                            f |= par & 1;
+                        }
+                    }
+                }
+                const int any_fail = __ballot(f) != 0ull;
+                if (lane == 0) {
+                    if (a.status) a.status[shot] = (uint8_t)(sw == 0 ? 2 : 0);
+                    if (a.ssf_steps) a.ssf_steps[shot] = steps;
+                    if (a.fail) a.fail[shot] = (uint8_t)any_fail;
+                }
+                wave_lds_sync();
+            } else if (DEFER && !conv) {
                 // hard decision by column for the SSF queue (slot order -> xh[column])
 #pragma unroll
                 for (int rv = 0; rv < RV; ++rv) xh[core.col_of(rv)] = (uint8_t)((X[rv] >> lane) & 1);

@@ -172,6 +172,8 @@ struct DevGraph {
     int opt_ssf_inc;       // 1: incremental workgroup SSF (ssf_inc_block_kernel); 0: the re-scanning one
     int opt_block_wg;      // > 0: workgroups per CU of the HBM-slice workgroup kernels (0: automatic)
     int opt_group_mb;      // > 0: HBM budget of the slot-group scratch in MiB (0: a quarter of free HBM)
+    int opt_ssf_fuse;      // 1: two-pass SSF decodes run SSF inside the compact BP kernel (no queue, no
+                           // second launch); 0: queue + ssf_lut_kernel
 };
 
 // SSF kernel choice of wave graphs (DevGraph::opt_ssf)
@@ -185,6 +187,7 @@ inline void default_options(DevGraph& g) {
     g.opt_ssf_inc = 1;
     g.opt_block_wg = 0;
     g.opt_group_mb = 0;
+    g.opt_ssf_fuse = 1;
 }
 
 struct DecodeArgs {

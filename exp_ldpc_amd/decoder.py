@@ -28,7 +28,7 @@ __all__ = ["Decoder", "parse_bp_method", "as_csr01", "OPTIONS", "DEFAULT_OPTIONS
 # every choice gives identical results, they exist for A/B measurements and so
 # tests keep each kernel path covered
 OPTIONS = {"compact": 1, "triage_it1": 2, "ssf": 3, "lds_kernel": 4, "group_kernel": 5, "ssf_inc": 6,
-           "block_wg": 7, "group_mb": 8}
+           "block_wg": 7, "group_mb": 8, "ssf_fuse": 9}
 SSF_KERNELS = {"auto": 0, "scan": 1, "scan_gather": 2, "scan_nosplit": 3}  # values of the "ssf" option
 # options applied to every Decoder built afterwards (tests patch this dict to
 # route pipelines that build their decoders internally through one kernel path)

@@ -259,7 +259,11 @@ int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int3
  *   QD_OPT_BLOCK_WG      0 (default) automatic, N > 0: workgroups per CU of the
  *                        HBM-slice workgroup BP kernel.
  *   QD_OPT_GROUP_MB      0 (default): a quarter of the free HBM, N > 0: N MiB for
- *                        the slot-group kernel's message scratch. */
+ *                        the slot-group kernel's message scratch.
+ *   QD_OPT_SSF_FUSE      1 (default): two-pass min-sum decodes with SSF run the
+ *                        table-driven SSF inside the compact BP kernel, right
+ *                        after a shot's BP fails (no queue, no second launch);
+ *                        0: BP-failed shots queued for ssf_lut_kernel. */
 #define QD_OPT_COMPACT 1
 #define QD_OPT_TRIAGE_IT1 2
 #define QD_OPT_SSF 3
@@ -268,6 +272,7 @@ int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int3
 #define QD_OPT_SSF_INC 6
 #define QD_OPT_BLOCK_WG 7
 #define QD_OPT_GROUP_MB 8
+#define QD_OPT_SSF_FUSE 9
 #define QD_SSF_AUTO 0
 #define QD_SSF_SCAN 1
 #define QD_SSF_SCAN_GATHER 2

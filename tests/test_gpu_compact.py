@@ -139,10 +139,13 @@ def test_compact_ssf_rpar_and_partial_outputs(gpu_available, oracle_lib, precisi
         ref = oracle_lib.decode(hz, 0.027, syn, method="ms", precision=precision, max_iter=30, ssf=True, gens=hx, lz=L,
                                 readout=rd, want_llr=False, ssf_impl="fast")
         assert ref["ssf_steps"].sum() > 0 and ref["fail"].any()
-        for kern, name in (("scan", "ssf_wave_kernel"), ("auto", "ssf_lut_kernel")):
+        # scanning kernel; table-driven kernel behind the queue; SSF fused into
+        # the compact BP kernel (QD_OPT_SSF_FUSE, the default: no SSF launch)
+        for kern, name, fuse in (("scan", "ssf_wave_kernel", 1), ("auto", "ssf_lut_kernel", 0), ("auto", "", 1)):
             dec.set_option("ssf", kern)
+            dec.set_option("ssf_fuse", fuse)
             got, (bp_k, ssf_k, _) = _decode_device(dec, syn, rd)
-            assert "cmp_kernel" in bp_k and name in ssf_k, (bp_k, ssf_k)
+            assert "cmp_kernel" in bp_k and (name in ssf_k if name else ssf_k == ""), (bp_k, ssf_k)
             for key in got:
                 assert np.array_equal(got[key], ref[key]), (extra, kern, key)
         part, _ = _decode_device(dec, syn, rd, keys=("fail",))
@@ -154,14 +157,17 @@ def test_compact_ssf_rpar_and_partial_outputs(gpu_available, oracle_lib, precisi
     assert np.array_equal(nofail["iters"], ref["iters"]) and np.array_equal(nofail["status"], ref["status"])
 
 
-def test_compact_large_batch_counter_tail(gpu_available, oracle_lib, code225):
+@pytest.mark.parametrize("fuse", [1, 0])
+def test_compact_large_batch_counter_tail(gpu_available, oracle_lib, code225, fuse):
     """2^18 shots at p = 0.05 (a compact list long enough for the chunk counter's
-    dynamic tail): a random subset of 3000 shots equals the oracle."""
+    dynamic tail; most BP failures go to SSF, fused into the BP kernel or through
+    the queue): a random subset of 3000 shots equals the oracle."""
     import torch
     from exp_ldpc_amd.decoder import Decoder
     hz, hx, lz = code225.checks.z, code225.checks.x, code225.logicals.z
     B, p = 1 << 18, 0.05
     dec = Decoder(hz, 2 * p / 3, method="ms", precision="f64", max_iter=50, flip_sets=hx, logicals=lz)
+    dec.set_option("ssf_fuse", fuse)
     dev = torch.device("cuda", 0)
     syn = torch.empty((B, hz.shape[0]), dtype=torch.uint8, device=dev)
     rd = torch.empty((B, hz.shape[1]), dtype=torch.uint8, device=dev)

@@ -91,7 +91,7 @@ def test_packed_ragged_batches_and_padding_bits(gpu_available, oracle_lib, B):
     m, n = hz.shape
     rng = np.random.default_rng(B)
     rr = (rng.random((B, n)) < 0.02).astype(np.uint8)
-    rs = ((hz @ ((rr ^ (rng.random((B, n)) < 0.01)).T)).T % 2).astype(np.uint8)
+    rs = np.ascontiguousarray(((hz @ ((rr ^ (rng.random((B, n)) < 0.01)).T)).T % 2).astype(np.uint8))
     sw, rw = pack_rows(rs), pack_rows(rr)
     sw[:, -1] |= np.uint64(0xFFFF) << np.uint64(m % 64)   # m = 108: bits 44..59 are padding
     rw[:, -1] |= np.uint64(1) << np.uint64(63)            # n = 225: bit 63 of word 3 is padding
@@ -124,7 +124,7 @@ def test_packed_inputs_on_expanding_paths(gpu_available, oracle_lib):
     B = 700
     rr = (rng.random((B, n)) < 0.03).astype(np.uint8)
     base = (rng.random((B, n)) < 0.01).astype(np.uint8)
-    rs = ((hz @ rr.T).T % 2).astype(np.uint8)
+    rs = np.ascontiguousarray(((hz @ rr.T).T % 2).astype(np.uint8))
     want = ("x", "corr", "llr", "iters", "status", "ssf_steps", "fail")
     for method in ("ms", "ps"):
         dec = Decoder(hz, 0.02, method=method, precision="f64", max_iter=30, flip_sets=hx, logicals=lz)
@@ -151,7 +151,7 @@ def test_packed_inputs_on_expanding_paths(gpu_available, oracle_lib):
     hx4, hz4 = load_checks("hgp_80_3_4_s2025")
     dec4 = Decoder(hz4, 0.01, method="ms", precision="f32", max_iter=50, flip_sets=hx4)
     e4 = (rng.random((96, hz4.shape[1])) < 0.01).astype(np.uint8)
-    s4 = ((hz4 @ e4.T).T % 2).astype(np.uint8)
+    s4 = np.ascontiguousarray(((hz4 @ e4.T).T % 2).astype(np.uint8))
     a = dec4.decode(s4, want=("x", "iters", "status", "ssf_steps"))
     b = dec4.decode(pack_rows(s4), want=("x", "iters", "status", "ssf_steps"), packed=True)
     for k in a:

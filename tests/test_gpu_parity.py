@@ -437,8 +437,18 @@ def lean_path(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["fused", "queue"])
+def ssf_path(request, monkeypatch):
+    """Two-pass SSF decodes run SSF inside the compact BP kernel by default
+    (QD_OPT_SSF_FUSE = 1); 0 queues BP-failed shots for ssf_lut_kernel."""
+    from exp_ldpc_amd import decoder
+    if request.param == "queue":
+        monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "ssf_fuse", 0)
+    return request.param
+
+
 @pytest.mark.parametrize("precision,occupancy", [("f64", 0), ("f64", 12), ("f32", 0)])
-def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occupancy, lean_path):
+def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occupancy, lean_path, ssf_path):
     """The benchmarked instantiation (bp_ms_wave_kernel<.., LEAN=true, ..>, chosen
     when x / corr / llr are all null) pinned bit-exactly: exactly bench.py's
     decode_device call (syn + readout in; iters, status, ssf_steps, fail out) at
@@ -464,8 +474,11 @@ def test_bench_lean_kernels_all_points(gpu_available, oracle_lib, precision, occ
                (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
         dec.decode_device(B, syn=syn, readout=rd, **out)
         torch.cuda.synchronize()
-        bp_k, _, pre_k = dec.last_kernels()
+        bp_k, ssf_k, pre_k = dec.last_kernels()
         assert ("cmp_kernel" in bp_k and "triage" in pre_k) == (lean_path == "compact"), (bp_k, pre_k)
+        # fused: no SSF launch, the compact kernel's FUSE argument is the generators per lane
+        fused = lean_path == "compact" and ssf_path == "fused"
+        assert (ssf_k == "") == fused and (bp_k.endswith(", 2>") if fused else True), (bp_k, ssf_k)
         rs, rr = oracle_lib.sample_storage(hz, 0, p, p, seed=seed, stream=pi, shot0=shot0, B=B)
         assert np.array_equal(syn.cpu().numpy(), rs) and np.array_equal(rd.cpu().numpy(), rr), p
         ref = oracle_lib.decode(hz, 2 * p / 3, rs, method="ms", precision=precision, max_iter=50, ssf=True, gens=hx,
