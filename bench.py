@@ -885,7 +885,7 @@ def main():
                          "and roofline, every config line; the stdout line names it")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 line (c3_line; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--ssf-fuse", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--ssf-fuse", type=int, default=0, choices=[0, 1],
                     help="1: SSF inside the compact BP kernel (QD_OPT_SSF_FUSE); 0: queue + ssf_lut_kernel")
     # diagnostic: decode without SSF (prices SSF inside the overlapped step)
     ap.add_argument("--no-ssf-exp", action="store_true", help=argparse.SUPPRESS)

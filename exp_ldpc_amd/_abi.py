@@ -89,6 +89,7 @@ SIGNATURES = {
     "qd_graph_ssf_tables_copy": (_i32, [_p, _p, _p, _p, _p, C.POINTER(_i32), C.POINTER(_i32)]),
     "qd_graph_queue_layout": (_i32, [_p, _i64, _p]),
     "qd_graph_it1_tables_copy": (_i32, [_p, _i32, _p, _p, C.POINTER(_i32)]),
+    "qd_graph_lds64_slots_copy": (_i32, [_p, _p, _p]),
     "qd_graph_hgp_info": (_i32, [_p, _p]),
     "qd_graph_hgp_set_slots": (_i32, [_p, _i32]),
     "qd_graph_hgp_source": (_i64, [_p, C.c_char_p, _i64]),

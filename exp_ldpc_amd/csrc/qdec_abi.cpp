@@ -175,6 +175,113 @@ void ws_drain(qd_graph* G) {
 // seeded hill climb over position swaps drives every instruction to <= 2-way
 // conflicts (tie-break: sum of squared loads).  Pad lanes of an instruction all
 // write one dummy element, placed in the least-loaded bank.
+// Check-state slots of bp_ms_lds64_kernel (f64, one shot per CU; qdec_bp_block.hip).
+// Its variable thread t owns columns r * 1024 + (67 t mod 1024); per (wave,
+// round r, edge k) one LDS instruction of 64 lanes reads or atomically updates
+// the state of each lane's k-th check: u64 m1 / m2 elements (ds_read_b64,
+// ds_min_u64: bank pair = slot mod 32 per 32-lane half) and bit words
+// (parw / hdw / tiew: word = slot >> 5, bank = word mod 32).  With checks in
+// their natural order a half's 32 lanes land on ~3-4 lanes per bank (the PMC
+// of round 5: 0.61 of the kernel's LDS cycles were bank conflicts).  A seeded
+// anneal over slot swaps spreads every half over the banks (objective: sum of
+// squared lanes per bank, both keys; tools/dev/c4_bank_model.py's max-per-bank
+// model on C4: 22,975 -> ~14,600 cycles, ideal 7,072).  The kernel then works in
+// slot space; m64_check maps a slot back to its check for the syndrome input and
+// the residual output.  Cached per process like ms_layout.
+void m64_layout(qd_graph* G, int m, int n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
+                const std::vector<int>& edge_cpos) {
+    DevGraph& g = G->dg;
+    struct Entry {
+        std::vector<int32_t> rp, ci;
+        std::vector<uint16_t> et, chk;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const auto& c : cache)
+            if (c.rp == rp && c.ci == ci) {
+                g.m64_etab = G->arena.upload(c.et);
+                g.m64_check = G->arena.upload(c.chk);
+                return;
+            }
+    }
+    constexpr int T = 1024;  // kM64Threads
+    const int E = rp[m];
+    // k-th check of every column (edge_cpos order, as ml_etab)
+    std::vector<int> colchk((size_t)kMlDC * n, -1);
+    for (int i = 0; i < m; ++i)
+        for (int e = rp[i]; e < rp[i + 1]; ++e)
+            if (edge_cpos[e] < kMlDC) colchk[(size_t)edge_cpos[e] * n + ci[e]] = i;
+    // the halves: 32 lanes of one instruction; occurrences of each check
+    std::vector<std::vector<int>> halves;
+    const int rounds = (n + T - 1) / T;
+    for (int w = 0; w < T / 64; ++w)
+        for (int r = 0; r < rounds; ++r)
+            for (int k = 0; k < kMlDC; ++k)
+                for (int h = 0; h < 2; ++h) {
+                    std::vector<int> hh;
+                    for (int l = 32 * h; l < 32 * h + 32; ++l) {
+                        const int j = r * T + ((64 * w + l) * 67) % T;
+                        if (j < n && colchk[(size_t)k * n + j] >= 0) hh.push_back(colchk[(size_t)k * n + j]);
+                    }
+                    if (!hh.empty()) halves.push_back(std::move(hh));
+                }
+    const int nh = (int)halves.size();
+    std::vector<std::vector<int>> occ(m);
+    for (int h = 0; h < nh; ++h)
+        for (int i : halves[h]) occ[i].push_back(h);
+    std::vector<int> slot(m);
+    for (int i = 0; i < m; ++i) slot[i] = i;
+    std::vector<int> cx((size_t)nh * 32, 0), cy((size_t)nh * 32, 0);
+    auto X = [](int s) { return s & 31; };
+    auto Y = [](int s) { return (s >> 5) & 31; };
+    for (int h = 0; h < nh; ++h)
+        for (int i : halves[h]) ++cx[(size_t)h * 32 + X(slot[i])], ++cy[(size_t)h * 32 + Y(slot[i])];
+    const double WX = 5.0, WY = 1.5;  // u64 state ops outnumber the bit-word ops
+    auto move = [&](int i, int from, int to) {
+        for (int h : occ[i]) {
+            --cx[(size_t)h * 32 + X(from)], --cy[(size_t)h * 32 + Y(from)];
+            ++cx[(size_t)h * 32 + X(to)], ++cy[(size_t)h * 32 + Y(to)];
+        }
+    };
+    auto local = [&](int i, int s) {  // check i's share of the squared loads at slot s
+        double c = 0;
+        for (int h : occ[i]) c += WX * (2 * cx[(size_t)h * 32 + X(s)] - 1) + WY * (2 * cy[(size_t)h * 32 + Y(s)] - 1);
+        return c;
+    };
+    std::mt19937_64 rng(20250221);
+    std::uniform_real_distribution<double> uni(0.0, 1.0);
+    const long iters = m > 1 ? std::min<long>(6000000L, 1500L * E) : 0;
+    const double T0 = 1.0, T1 = 0.01;
+    for (long it = 0; it < iters; ++it) {
+        const int i = (int)(rng() % (uint64_t)m), j = (int)(rng() % (uint64_t)m);
+        const int si = slot[i], sj = slot[j];
+        if (i == j || (X(si) == X(sj) && Y(si) == Y(sj))) continue;
+        const double before = local(i, si) + local(j, sj);
+        move(i, si, sj);
+        move(j, sj, si);
+        const double d = local(i, sj) + local(j, si) - before;
+        const double temp = T0 * std::pow(T1 / T0, (double)it / (double)iters);
+        if (d <= 0 || uni(rng) < std::exp(-d / temp)) {
+            slot[i] = sj;
+            slot[j] = si;
+        } else {
+            move(j, si, sj);
+            move(i, sj, si);
+        }
+    }
+    Entry e{rp, ci, std::vector<uint16_t>((size_t)kMlDC * n, 0xffff), std::vector<uint16_t>(m)};
+    for (size_t t = 0; t < colchk.size(); ++t)
+        if (colchk[t] >= 0) e.et[t] = (uint16_t)slot[colchk[t]];
+    for (int i = 0; i < m; ++i) e.chk[slot[i]] = (uint16_t)i;
+    g.m64_etab = G->arena.upload(e.et);
+    g.m64_check = G->arena.upload(e.chk);
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 8) cache.erase(cache.begin());
+    cache.push_back(std::move(e));
+}
+
 void ms_layout(qd_graph* G, int m, int n, const std::vector<int>& edge_cpos) {
     DevGraph& g = G->dg;
     const auto& rp = G->row_ptr;
@@ -687,6 +794,8 @@ void build_tables(qd_graph* G, int m, int n) {
         // LDS-resident min-sum kernel (bp_ms_lds_kernel): edge k of column j (CSC
         // order) lives at LDS element row * kMlDRS + position in the CSR row
         g.ml_etab = nullptr;
+        g.m64_etab = nullptr;
+        g.m64_check = nullptr;
         if (g.max_rdeg <= kMlDRS && g.max_cdeg <= kMlDC && (size_t)m * kMlDRS + 64 < 0xffff) {
             const std::vector<int> pos = ml_positions(m, n, rp, ci, edge_cpos);
             std::vector<uint16_t> et((size_t)kMlDC * n, 0xffff);
@@ -694,6 +803,7 @@ void build_tables(qd_graph* G, int m, int n) {
                 for (int e = rp[i]; e < rp[i + 1]; ++e)
                     et[(size_t)edge_cpos[e] * n + ci[e]] = (uint16_t)(i * kMlDRS + pos[e]);
             g.ml_etab = G->arena.upload(et);
+            m64_layout(G, m, n, rp, ci, edge_cpos);
         }
         return;
     }
@@ -1997,6 +2107,17 @@ int qd_graph_it1_tables_copy(const qd_graph* G, int32_t precision, uint16_t* lut
         if (!g.it1_lut[precision] || !g.it1_vchk) throw Fail(-37, "no iteration-1 tables for this precision");
         if (lut) std::memcpy(lut, g.it1_lut[precision], (size_t)g.n_pad * 2);
         if (vchk) std::memcpy(vchk, g.it1_vchk, (size_t)g.n_pad * 8);
+    });
+}
+
+int qd_graph_lds64_slots_copy(const qd_graph* G, uint16_t* etab, uint16_t* check_of_slot) {
+    return guarded([&] {
+        check_graph(G);
+        if (!G->host_only) throw Fail(-16, "table copies are kept for host-only graphs (qd_graph_create_host)");
+        const DevGraph& g = G->dg;
+        if (!g.m64_etab || !g.m64_check) throw Fail(-38, "no f64 LDS-kernel slot tables for this graph");
+        if (etab) std::memcpy(etab, g.m64_etab, (size_t)kMlDC * g.n * 2);
+        if (check_of_slot) std::memcpy(check_of_slot, g.m64_check, (size_t)g.m * 2);
     });
 }
 

@@ -1006,13 +1006,20 @@ static int launch_triage(const DevGraph& g, const DecodeArgs& a, hipStream_t str
     const size_t it1 = a.it1_lut ? TriageIt1<RC, RV>::bytes : 0;
     const size_t lds = ((want_fail ? (size_t)g.k * g.lz_words * 8 : 0) + 15) / 16 * 16 +
                        tiles + it1;
+    const void* fn = a.in_packed ? reinterpret_cast<const void*>(ms_triage_kernel<RC, RV, true>)
+                                 : reinterpret_cast<const void*>(ms_triage_kernel<RC, RV, false>);
     if (lds > 64 * 1024) {  // large logical tables (k <= 256, lz_words <= 9)
-        const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(ms_triage_kernel<RC, RV>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const hipError_t ea = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ea != hipSuccess) return (int)ea;
     }
-    QDEC_NOTE_PRE("qdec::ms_triage_kernel", RC, RV);
-    hipLaunchKernelGGL((ms_triage_kernel<RC, RV>), dim3((unsigned)((a.B + 63) / 64)), dim3(64), lds, stream, g, a);
+    const dim3 grid((unsigned)((a.B + 63) / 64));
+    if (a.in_packed) {
+        QDEC_NOTE_PRE("qdec::ms_triage_kernel", RC, RV, true);
+        hipLaunchKernelGGL((ms_triage_kernel<RC, RV, true>), grid, dim3(64), lds, stream, g, a);
+    } else {
+        QDEC_NOTE_PRE("qdec::ms_triage_kernel", RC, RV, false);
+        hipLaunchKernelGGL((ms_triage_kernel<RC, RV, false>), grid, dim3(64), lds, stream, g, a);
+    }
     return (int)hipGetLastError();
 }
 

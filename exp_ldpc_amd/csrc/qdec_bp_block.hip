@@ -1467,10 +1467,15 @@ __host__ __device__ inline size_t m64_lds_bytes(const DevGraph& g) {
 
 __device__ __forceinline__ unsigned long long dbits(double x) { return (unsigned long long)__double_as_longlong(x); }
 
+// The check states live at host-placed slots (DevGraph::m64_etab / m64_check,
+// m64_layout in qdec_abi.cpp: a wave's state accesses spread over the LDS
+// banks); every array below is indexed by slot, and the syndrome input and the
+// residual output go through cslot (slot -> check).
 template <int VPT>
 __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, DecodeArgs a,
                                                                  const uint16_t* __restrict__ etab,
-                                                                 const double* __restrict__ prior) {
+                                                                 const double* __restrict__ prior,
+                                                                 const uint16_t* __restrict__ cslot) {
     static_assert(VPT * 3 <= 32 && VPT <= 32, "degree and decision bits");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     long long* next = reinterpret_cast<long long*>(smem + 56);
@@ -1515,8 +1520,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 e1 = etab[(size_t)(2 * h + 1) * n + j];
             }
             dj += (e0 != 0xffffu) + (e1 != 0xffffu);
-            e0 = e0 == 0xffffu ? 0u : e0 / kMlDRS;
-            e1 = e1 == 0xffffu ? 0u : e1 / kMlDRS;
+            e0 = e0 == 0xffffu ? 0u : e0;  // state slots (m64_etab)
+            e1 = e1 == 0xffffu ? 0u : e1;
             ep[r][h] = e0 | (e1 << 16);
         }
         djs |= (uint32_t)dj << (3 * r);
@@ -1565,11 +1570,11 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
         __syncthreads();
         const int64_t shot = *next;
         if (shot >= a.B) break;
-        // ---- S: syndrome words (ballots of 64 consecutive checks), both buffers reset
-        uint32_t sb = 0;  // syndrome bits of the owned checks
+        // ---- S: syndrome words (ballots of 64 consecutive slots), both buffers reset
+        uint32_t sb = 0;  // syndrome bits of the owned slots
         for (int c = 0; c < nch; ++c) {
             const int i = c * kM64Threads + tid;
-            const uint32_t s = i < m ? (uint32_t)(a.syn[shot * m + i] & 1) : 0u;
+            const uint32_t s = i < m ? (uint32_t)(a.syn[shot * m + cslot[i]] & 1) : 0u;
             sb |= s << c;
             const unsigned long long bw = __ballot(s != 0u);
             const int w0 = (c * kM64Threads + wv * 64) >> 5;
@@ -1708,7 +1713,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             const int j = r * kM64Threads + tq;
             if (j < n) a.q_x[shot * n + j] = (uint8_t)((xb >> r) & 1);
         }
-        for (int c = 0; c < ncr; ++c) a.q_r[shot * m + c * kM64Threads + tid] = (uint8_t)((bad >> c) & 1);
+        for (int c = 0; c < ncr; ++c) a.q_r[shot * m + cslot[c * kM64Threads + tid]] = (uint8_t)((bad >> c) & 1);
         if (tid == 0) {
             a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
             if (a.iters) a.iters[shot] = conv ? it : a.max_iter;
@@ -1852,7 +1857,7 @@ static int launch_block_typed(const DevGraph& g, const DecodeArgs& a0, int num_c
 // LDS budget); by default they take the min-sum graphs whose messages would go
 // to HBM (f32: edge slots <= 160 KB; f64: n <= 10240 and the check states <= 160 KB).
 bool lds_kernel_applies(const DevGraph& g, int method, int precision, const DecodeArgs& a) {
-    if (method != 1 || !g.ml_etab) return false;
+    if (method != 1 || !g.ml_etab || (precision == 0 && (!g.m64_etab || !g.m64_check))) return false;
     if (!a.syn || a.syn_flags || a.llr_out || !a.wave_ctr) return false;
     if (precision == 0) {  // bp_ms_lds64_kernel (automatic: graphs whose messages would go to HBM)
         if (g.n > 10 * kM64Threads || g.m <= 0 || g.m > 32 * kM64Threads || a.max_iter < 1) return false;
@@ -1911,7 +1916,7 @@ static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     record_ev(a, 0, stream);
     QDEC_NOTE_BP("qdec::bp_ms_lds64_kernel", VPT);
     hipLaunchKernelGGL((bp_ms_lds64_kernel<VPT>), dim3((unsigned)grid), dim3(kM64Threads), lds, stream, g, a,
-                       g.ml_etab, reinterpret_cast<const double*>(g.prior[1][0]));
+                       g.m64_etab, reinterpret_cast<const double*>(g.prior[1][0]), g.m64_check);
     const hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;

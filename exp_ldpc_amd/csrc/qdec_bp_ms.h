@@ -853,8 +853,11 @@ __host__ __device__ inline size_t triage_img_bytes(int64_t len) {
     return (size_t)((2 * (nch + 8) + 15) / 16 * 16);
 }
 
-// One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).
-template <int RC, int NWD>
+// One wave per tile of 64 shots (lane l = shot 64 * blockIdx.x + l).  PK:
+// bit-packed input rows (QD_INPUT_PACKED; a.in_packed), read as u64 words, no
+// tile images (its own instantiation: the byte path's 16-B tile loads keep ~100
+// VGPRs in flight, which the packed path does not need).
+template <int RC, int NWD, bool PK = false>
 __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs a) {
     using Ent = CmpEntry<RC>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -876,7 +879,7 @@ __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs
     // row_bits reads one dword past a row)
     uint64_t* lz_lds = reinterpret_cast<uint64_t*>(smem);
     const int nlz = want_fail ? g.k * g.lz_words : 0;
-    const bool pk = a.in_packed != 0;  // bit-packed input rows: no tile images
+    constexpr bool pk = PK;  // bit-packed input rows: no tile images
     unsigned char* syn_img = smem + ((size_t)nlz * 8 + 15) / 16 * 16;
     unsigned char* rd_img = syn_img + (pk ? 0 : triage_img_bytes(64 * (int64_t)m));
     // iteration-1 words: past the images
@@ -901,7 +904,7 @@ __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs
     const int64_t shot = s0 + lane;
     uint64_t sw[RC];
     uint64_t rw[NWD];
-    if (pk) {
+    if constexpr (PK) {
         // one row of u64 words per shot (RC = ceil(m / 64), NWD = ceil(n_data / 64)
         // on wave graphs): lane-strided loads, padding bits cleared
         const uint64_t* sp = reinterpret_cast<const uint64_t*>(a.syn) + min(shot, a.B - 1) * RC;

@@ -107,6 +107,11 @@ struct DevGraph {
     // [kMlDC][n] LDS element of edge k of column j (row * kMlDRS + CSR position),
     // pad 0xffff; nullptr when the graph's degrees exceed kMlDRS / kMlDC
     const uint16_t* ml_etab;
+    // bp_ms_lds64_kernel: check states live at host-placed slots (m64_layout,
+    // qdec_abi.cpp): [kMlDC][n] state slot of edge k of column j (pad 0xffff),
+    // and [m] the check held by each slot
+    const uint16_t* m64_etab;
+    const uint16_t* m64_check;
     // flip sets (SSF)
     int n_gen, g_pad, g_wmax;
     const uint8_t* g_w;           // [g_pad]
@@ -173,7 +178,7 @@ struct DevGraph {
     int opt_block_wg;      // > 0: workgroups per CU of the HBM-slice workgroup kernels (0: automatic)
     int opt_group_mb;      // > 0: HBM budget of the slot-group scratch in MiB (0: a quarter of free HBM)
     int opt_ssf_fuse;      // 1: two-pass SSF decodes run SSF inside the compact BP kernel (no queue, no
-                           // second launch); 0: queue + ssf_lut_kernel
+                           // second launch); 0 (default): queue + ssf_lut_kernel
 };
 
 // SSF kernel choice of wave graphs (DevGraph::opt_ssf)
@@ -187,7 +192,7 @@ inline void default_options(DevGraph& g) {
     g.opt_ssf_inc = 1;
     g.opt_block_wg = 0;
     g.opt_group_mb = 0;
-    g.opt_ssf_fuse = 1;
+    g.opt_ssf_fuse = 0;  // measured: 2x the separate SSF kernel's time at p = 0.1 (profiles/r06c)
 }
 
 struct DecodeArgs {

@@ -260,10 +260,11 @@ int qd_graph_last_kernels(qd_graph* g, char* bp, int32_t bp_len, char* ssf, int3
  *                        HBM-slice workgroup BP kernel.
  *   QD_OPT_GROUP_MB      0 (default): a quarter of the free HBM, N > 0: N MiB for
  *                        the slot-group kernel's message scratch.
- *   QD_OPT_SSF_FUSE      1 (default): two-pass min-sum decodes with SSF run the
- *                        table-driven SSF inside the compact BP kernel, right
- *                        after a shot's BP fails (no queue, no second launch);
- *                        0: BP-failed shots queued for ssf_lut_kernel. */
+ *   QD_OPT_SSF_FUSE      0 (default): BP-failed shots of two-pass min-sum decodes
+ *                        are queued for ssf_lut_kernel; 1: the compact BP kernel
+ *                        runs the same table-driven SSF itself right after a
+ *                        shot's BP fails (no queue, no second launch; its tables
+ *                        come through the caches, not LDS: measured slower). */
 #define QD_OPT_COMPACT 1
 #define QD_OPT_TRIAGE_IT1 2
 #define QD_OPT_SSF 3
@@ -306,6 +307,10 @@ int qd_graph_queue_layout(const qd_graph* g, int64_t B, int64_t* out);
  * vchk[n_pad] (the checks of column j's edges, 4 x u16, pad = m).  Fails when
  * the precision has no tables (a prior <= 0).  No reference counterpart. */
 int qd_graph_it1_tables_copy(const qd_graph* g, int32_t precision, uint16_t* lut, uint64_t* vchk, int32_t* n_pad);
+/* Host-only graphs: the f64 LDS-resident kernel's check-state slots (m64_layout):
+ * etab uint16 [4][n] (slot of edge k of column j, 0xffff pad), check_of_slot
+ * uint16 [m].  -38 when the graph has none.  For tests. */
+int qd_graph_lds64_slots_copy(const qd_graph* g, uint16_t* etab, uint16_t* check_of_slot);
 
 int qd_graph_ssf_tables_copy(const qd_graph* g, uint32_t* lut, uint32_t* off, uint32_t* lcw, uint32_t* tog,
                              int32_t* g_pad, int32_t* m_pad);

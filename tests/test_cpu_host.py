@@ -630,3 +630,56 @@ def test_pack_rows_layout():
         pb = np.packbits(a, axis=1, bitorder="little")
         assert np.array_equal(by[:, :pb.shape[1]], pb) and not by[:, pb.shape[1]:].any()
         assert np.array_equal(unpack_rows(w, L), a)
+
+
+def _m64_model(slot_of, halves):
+    """tools/dev/c4_bank_model.py's cost: per 32-lane half, the most lanes on one
+    bank for u64 state ops (slot mod 32; weight 5) and bit-word ops ((slot >> 5)
+    mod 32; weight 1.5)."""
+    c = 0.0
+    for hh in halves:
+        s = slot_of[hh]
+        c += 5.0 * np.bincount(s % 32, minlength=32).max() + 1.5 * np.bincount((s >> 5) % 32, minlength=32).max()
+    return c
+
+
+def test_lds64_state_slots_spread_the_banks():
+    """bp_ms_lds64_kernel's check-state slots (m64_layout) on the C4 code: a
+    permutation of the checks whose edge table is the checks' slots, and which
+    lowers the bank model of the kernel's per-instruction state accesses by a
+    third against the natural order (the GPU tests pin the decode itself)."""
+    import ctypes as C
+
+    from exp_ldpc_amd import _abi
+    lib = _abi.load()
+    hx, hz = load_checks("hgp_80_3_4_s2025")
+    H = sp.csr_matrix(hz)
+    m, n = H.shape
+    h, _, _ = _host_graph(lib, H)
+    et = np.zeros(4 * n, np.uint16)
+    chk = np.zeros(m, np.uint16)
+    _abi.check(lib.qd_graph_lds64_slots_copy(h, _abi.ptr(et), _abi.ptr(chk)), "lds64 slots")
+    lib.qd_graph_destroy(h)
+    assert np.array_equal(np.sort(chk), np.arange(m))
+    slot_of = np.empty(m, np.int64)
+    slot_of[chk] = np.arange(m)
+    Hc = H.tocsc()
+    Hc.sort_indices()
+    et = et.reshape(4, n)
+    colchk = np.full((4, n), -1)
+    for j in range(n):
+        rows = Hc.indices[Hc.indptr[j]:Hc.indptr[j + 1]]
+        colchk[:rows.size, j] = rows
+        assert np.array_equal(et[:rows.size, j], slot_of[rows]) and (et[rows.size:, j] == 0xFFFF).all()
+    halves = []
+    for w in range(16):
+        for r in range((n + 1023) // 1024):
+            for k in range(4):
+                for hf in range(2):
+                    js = [r * 1024 + ((64 * w + l) * 67) % 1024 for l in range(32 * hf, 32 * hf + 32)]
+                    cs = [colchk[k, j] for j in js if j < n and colchk[k, j] >= 0]
+                    if cs:
+                        halves.append(np.array(cs))
+    natural = _m64_model(np.arange(m), halves)
+    placed = _m64_model(slot_of, halves)
+    assert placed < 0.75 * natural, (placed, natural)

@@ -439,11 +439,10 @@ def lean_path(request, monkeypatch):
 
 @pytest.fixture(params=["fused", "queue"])
 def ssf_path(request, monkeypatch):
-    """Two-pass SSF decodes run SSF inside the compact BP kernel by default
-    (QD_OPT_SSF_FUSE = 1); 0 queues BP-failed shots for ssf_lut_kernel."""
+    """Two-pass SSF decodes queue BP-failed shots for ssf_lut_kernel by default
+    (QD_OPT_SSF_FUSE = 0); 1 runs SSF inside the compact BP kernel."""
     from exp_ldpc_amd import decoder
-    if request.param == "queue":
-        monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "ssf_fuse", 0)
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "ssf_fuse", 1 if request.param == "fused" else 0)
     return request.param
 
 
