@@ -104,6 +104,10 @@ struct qd_graph {
     // byte rows (grow only; DecodeArgs::unpack_buf)
     void* ubuf = nullptr;
     size_t ubuf_bytes = 0;
+    // compact-list segment counters, two sets (DecodeArgs::cmp_count_next):
+    // two-pass decodes alternate between them, each triage zeroing the other
+    void* cmpc = nullptr;
+    int cmp_par = 0;
     size_t mws_failed = 0;  // smallest scratch size whose allocation failed (0: none)
     uint64_t mws_capped_calls = 0;  // calls served the reduced scratch since the failure
     // kernel timing ring (qd_graph_set_timing): 3 events per decode call
@@ -917,7 +921,24 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
         a.cmp_count = reinterpret_cast<unsigned long long*>(base + L.cmp_count);
         a.cmp = reinterpret_cast<uint64_t*>(base + L.cmp);
         a.cmp_cap = L.cmp_cap;
+        // double-buffered counters (zeroed once here, then by each triage for
+        // the next decode): no memset launch per decode
+        const size_t set = (size_t)kCmpLists * kCmpSegs * 128;
+        if (!G->cmpc) {
+            hip_check(hipMalloc(&G->cmpc, 2 * set), "hipMalloc list counters");
+            hip_check(hipMemset(G->cmpc, 0, 2 * set), "hipMemset list counters");
+            G->cmp_par = 0;
+        }
+        auto* c = static_cast<uint8_t*>(G->cmpc);
+        a.cmp_count = reinterpret_cast<unsigned long long*>(c + (size_t)G->cmp_par * set);
+        a.cmp_count_next = reinterpret_cast<unsigned long long*>(c + (size_t)(G->cmp_par ^ 1) * set);
     }
+}
+
+// after a launch: a two-pass decode (its triage ran) used one counter set and
+// zeroed the other, so the next one takes the other set
+void flip_counters(qd_graph* G, const DecodeArgs& a) {
+    if (a.cmp_count_next && !G->last_pre.empty()) G->cmp_par ^= 1;
 }
 
 void* message_scratch(qd_graph* G, int method, int precision, const DecodeArgs& a, size_t* bytes) {
@@ -1327,6 +1348,7 @@ int qd_graph_destroy(qd_graph* g) {
         if (g->qws) (void)hipFree(g->qws);
         if (g->mws) (void)hipFree(g->mws);
         if (g->ubuf) (void)hipFree(g->ubuf);
+        if (g->cmpc) (void)hipFree(g->cmpc);
         if (g->ctl) (void)hipFree(g->ctl);
         hgp_plan_destroy(g->hgp);
         free_timing(g);
@@ -1750,6 +1772,7 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         ws_acquire(G, s);
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
+        flip_counters(G, a);  // also after a failed BP launch: its triage zeroed the other set
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         note_listed(G, a, s, split ? G->ssf_stream : s);
         // the last user of the queue is the SSF kernel: the workspace chain
@@ -1815,6 +1838,7 @@ int qd_decode_batch(qd_graph* G, const qd_params* p, int64_t B, const uint8_t* s
         ws_acquire(G, s);
         const int rc = launch_decode(g, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
+        flip_counters(G, a);  // also after a failed BP launch: its triage zeroed the other set
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
         note_listed(G, a, s, s);
         ws_release(G, s);

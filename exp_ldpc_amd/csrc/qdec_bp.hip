@@ -1048,8 +1048,10 @@ static int launch_bp_wave(const DevGraph& g, const DecodeArgs& a, int num_cus, h
             b.it1_lut = (a.ms_scaling == 0.0 && a.max_iter >= 1 && g.opt_triage_it1)
                             ? g.it1_lut[sizeof(T) == 4 ? 1 : 0]
                             : nullptr;
-            hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpLists * kCmpSegs * 128, stream);
-            if (e != hipSuccess) return (int)e;
+            if (!b.cmp_count_next) {  // double-buffered counters arrive zeroed (the previous triage)
+                const hipError_t e = hipMemsetAsync(b.cmp_count, 0, (size_t)kCmpLists * kCmpSegs * 128, stream);
+                if (e != hipSuccess) return (int)e;
+            }
             int rc = launch_triage<RC, RV>(g, b, stream);
             if (rc != 0) return rc;
             if (b.ev) (void)hipEventRecord(b.ev[3], stream);  // end of the pre-pass

@@ -874,6 +874,10 @@ __global__ __launch_bounds__(64, 1) void ms_triage_kernel(DevGraph g, DecodeArgs
         if (a.wave_ctr) a.wave_ctr[0] = a.wave_ctr[1] = 0ull;
         if (a.q_count) *a.q_count = 0;
     }
+    // the handle's other list-counter set, for its next two-pass decode (the
+    // decode that last used it has finished: the workspace chain orders them)
+    if (blockIdx.x == 0 && a.cmp_count_next)
+        for (int s = lane; s < kCmpLists * kCmpSegs; s += 64) a.cmp_count_next[16 * s] = 0ull;
     // LDS: the logicals (k x lz_words u64, read as broadcasts), then the
     // syndrome and readout tiles as 16-B chunk images (one spare chunk each:
     // row_bits reads one dword past a row)

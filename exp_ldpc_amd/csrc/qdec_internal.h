@@ -246,6 +246,10 @@ struct DecodeArgs {
     // counter; zeroed by the launcher).  nullptr -> no compact path
     uint64_t* cmp;
     unsigned long long* cmp_count;
+    // the other counter set of the handle (double-buffered): the triage zeroes
+    // it for the handle's next two-pass decode, so no decode needs a memset
+    // launch (nullptr: the launcher memsets cmp_count itself)
+    unsigned long long* cmp_count_next;
     int64_t cmp_cap;
     int cmp_zero_ok;  // every prior of the launch's precision > 0: zero syndromes finish in the triage
     // the triage runs iteration 1 itself (g.it1_lut of the launch's precision;
