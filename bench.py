@@ -12,7 +12,19 @@ Precision: the headline line (`value`, `dtype`) runs BP in f64, ldpc v1's
 message precision (its loops use double).  The same shots are then decoded in
 f32 (the stated-tolerance variant) and reported under `variants`.
 
-Phases (rank 0 prints ONE JSON line):
+Output: rank 0 prints ONE JSON line of at most LINE_MAX_BYTES (the driver's
+parser; round 5's 20 KB line was not read): the contract's fields, `roofline`,
+`cpu_baseline`, the LER curve as one row of failures per p (the reference's own
+record, misc/p_sweep.py:32-33) and one number + roofline fraction per extra
+config (`configs`: C3, C4 f32 / f64, C5, the reference default).  The full
+record (per-point roofline and LER, every config line, sub-records) goes to the
+side file the line names (`detail`, --detail-out).
+
+Inputs: the syndrome and readout rows are bit-packed u64 words by default
+(QD_INPUT_PACKED: 48 B per shot at n = 225 instead of 333; the sampler writes
+them, the triage reads them), --inputs bytes keeps one byte per bit.
+
+Phases:
   1. headline: W warmup + K timed steps, the 9 points round-robin over --streams
      HIP streams (default 9: every point on its own stream; measured 79 vs 76 M
      f64 shots/s at 5), so kernels of independent points fill each other's tails;
@@ -32,9 +44,13 @@ Phases (rank 0 prints ONE JSON line):
      roofline uses these (overlapped launches share the chip, so their durations
      are not one kernel's);
   4. sampling + decode: K steps with the sampler inside the timed region;
-  5. (rank 0, N = 1) `large_code_roofline`: the HBM-bound path, BASELINE config 5
-     (n = 53,040 Cayley-graph LP code, R = 1 spacetime syndromes) on the
-     slot-group kernel, one timed launch with its HBM roofline fraction.
+  5. (rank 0, N = 1) `c3_line`: BASELINE config 3 ([[144,12,12]] BB lift,
+     BP + SSF f64, 2^22 shots per p at p = 0.001 / 0.003 / 0.01);
+     `large_code_roofline`: the HBM-bound path, BASELINE config 5 (n = 53,040
+     Cayley-graph LP code, R = 1 spacetime syndromes) on the slot-group kernel,
+     at two points where it decodes and the all-fail bandwidth point;
+     `c4_line` (config 4's code, f64 and f32); `reference_default` (configs[0]'s
+     bposd path with its compiled CPU leg).
 
 Multi-GPU: `torchrun --nproc-per-node N bench.py --gpus N` (one process per
 GPU), or `python bench.py --gpus N`, which starts that torchrun as a child
@@ -112,12 +128,12 @@ def load_code():
         return read_quantum_code(f, validate_stabilizer_code=True)
 
 
-def pmc_ceilings(kernel: str):
+def pmc_ceilings(kernel: str, **meta):
     """Per-launch PMC figures of exactly `kernel` (rocprof's spelling with its
     template arguments, as Decoder.last_kernels() reports it) from the newest
     committed PMC summary that holds it (profiles/*_pmc_summary.json, written by
-    tools/pmc_summary.py from rocprofv3 --pmc passes of this bench command), or
-    None."""
+    tools/pmc_summary.py from rocprofv3 --pmc passes of this bench command, or of
+    one launch shape of it tagged by `meta`, e.g. c5_p=0.005), or None."""
     if not kernel:
         return None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
@@ -126,6 +142,9 @@ def pmc_ceilings(kernel: str):
             with open(f) as fh:
                 d = json.load(fh)
         except Exception:
+            continue
+        fm = d.get("meta", {})
+        if any(fm.get(key) != val for key, val in meta.items()):
             continue
         for name, k in d.get("kernels", {}).items():
             if name.split("(", 1)[0] == kernel and "derived" in k:
@@ -252,7 +271,7 @@ def cpu_baseline(code, ps, args):
     return res
 
 
-def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005)):
+def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005), warm_shots: int = 1 << 13):
     """HBM roofline of the genuinely HBM-bound path: BASELINE config 5 (PSL(2,16)
     Cayley-graph LP code, n = 53,040) at R = 1 spacetime syndromes (H_st
     48,960 x 130,560, E = 236,640), BP min-sum f64 max_iter 50 + fold + logical
@@ -262,7 +281,9 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005)):
     at R = 1 and the code decodes (k = 4080 logicals: at p = 0.002 the LER is
     already 0.74, profiles/r06a); the last (0.005) is the worst case where
     every shot runs all 50 iterations (LER ~1), kept as the bandwidth figure.
-    The warmup launch decodes 2^13 shots (module load, scratch sizing).
+    The warmup launch decodes 2^13 shots (module load, scratch sizing;
+    tools/gpu/lines_only.py --c5-warm-full makes it the timed launch's twin, so
+    a PMC pass's per-dispatch average is that launch's).
     Algorithmic bytes = 32 B per edge per shot-iteration (f64 v2c read + c2v
     write in the check pass, c2v read + v2c write in the column pass) + the
     per-shot I/O (syndrome, readout, outputs)."""
@@ -290,13 +311,12 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005)):
     status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
     fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
     kernel = "qdec::bp_group_kernel<double, 1, 8, 4>"
-    pmc = pmc_ceilings(kernel)
     lines = []
     for p in ps:
         dec.set_priors(np.full(n, 2 * p / 3))
         for b in range(2):
             sampler.sample_storage_device(1, p, p, SEED, 100, b * shots, shots, syn[b], rd[b])
-        warm = min(shots, 1 << 13)
+        warm = min(shots, warm_shots)
         dec.decode_device(warm, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
         torch.cuda.synchronize(dev)
         dec.set_timing(1)
@@ -315,10 +335,12 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005)):
                "ler": float(fail[1].to(torch.float64).mean().item()),
                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": algo}}
-        if pmc is not None and pmc[2].get("config_p") in (None, p):
+        pmc = pmc_ceilings(kernel, c5_p=p, c5_shots=shots)  # PMC passes of exactly this launch shape
+        if pmc is not None:
             src, name, k = pmc
             row["roofline"]["traffic"] = k["derived"].get("hbm_bytes_per_dispatch")
             row["roofline"]["traffic_source"] = src
+            row["roofline"]["hbm_frac_pmc"] = k["derived"].get("hbm_frac")
         lines.append(row)
     res = {"config": "C5 as named: PSL(2,16) Cayley-graph LP (lifted_product_code_pgl2(1,4,2,double_cover=False,"
                      "seed=1)), n=53040 k=4080, R=1 spacetime 48960x130560 E=236640, BP min-sum f64 max_iter 50, "

@@ -16,4 +16,4 @@ for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $CTRS -d "$R/$OUT/pass$i" -o run --output-format csv -- python3 bench.py "$@" > "$R/$OUT/pass$i.log" 2>&1
   echo "pass $i done"
 done
-python3 tools/pmc_summary.py "$R/$OUT" "$R/$OUT/summary.json"
+python3 tools/pmc_summary.py "$R/$OUT" "$R/$OUT/summary.json" ${PMC_META:-}

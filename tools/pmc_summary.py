@@ -1,6 +1,8 @@
 """Summarise rocprofv3 PMC passes (tools/pmc.sh output) per kernel.
 
-Usage: python tools/pmc_summary.py <pmc_dir> <out.json>
+Usage: python tools/pmc_summary.py <pmc_dir> <out.json> [key=value ...]
+(key=value pairs go to the summary's "meta", e.g. c5_p=0.005: bench.py matches
+a summary to the launch it describes by them)
 
 Per kernel: dispatch count, the mean of every counter per dispatch, and derived
 ceilings computed from counter sums over the kernel's dispatches, each against
@@ -106,6 +108,15 @@ def main():
         d["derived"] = dv
         kernels[k] = d
     res = {"source": src, "kernels": kernels}
+    meta = {}
+    for kv in sys.argv[3:]:
+        key, _, val = kv.partition("=")
+        try:
+            meta[key] = float(val)
+        except ValueError:
+            meta[key] = val
+    if meta:
+        res["meta"] = meta
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     for k, v in sorted(kernels.items()):

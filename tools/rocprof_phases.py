@@ -30,7 +30,7 @@ def main():
     out = sys.argv[3] if len(sys.argv) > 3 else None
     b = json.load(open(bench))
     rf = b["roofline"]
-    P = len(b["ler"])
+    P = len(b["ler"]["p"]) if "p" in b["ler"] else len(b["ler"])  # the stdout line or its side file
     W, K = b["warmup"], b["steps"]
     iso = rf["launches"] // P
     by = defaultdict(list)
@@ -45,8 +45,18 @@ def main():
         return {"dispatches": len(v), "avg_ms": sum(v) / len(v) if v else None, "sum_ms": sum(v)}
 
     roof = rf.get("kernel", "")
-    occ3 = any(k.split("(")[0].startswith(roof.rsplit(",", 1)[0]) and k.split("(")[0].endswith(", 3>")
-               for k in by) if roof else False
+    def targs(name):
+        head = name.split("(")[0]
+        return head.split("<", 1)[0], [t.strip() for t in head.split("<", 1)[1].rstrip(">").split(",")] \
+            if "<" in head else []
+
+    # the 3-waves-per-SIMD build of the roofline kernel: template argument OCC (7th) = 3
+    occ3 = False
+    if roof:
+        fam, ra = targs(roof)
+        if len(ra) >= 7:
+            cand = ra[:6] + ["3"] + ra[7:]
+            occ3 = any(targs(k) == (fam, cand) for k in by)
     for name, d in sorted(by.items()):
         if "qdec::" not in name:
             continue
