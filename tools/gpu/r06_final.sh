@@ -2,7 +2,7 @@
 # Round-6 evidence: GPU suite, smoke, default bench (+ side file), rocprofv3
 # kernel-trace stats of the same command and its phase split, PMC of the
 # headline kernels, C5 (decoding point and bandwidth point), C3 and C4 f64.
-# Usage: tools/gpu/r06_final.sh <tag> [skip-tests]
+# Usage: tools/gpu/r06_final.sh <tag> [skip-tests|tests] [no-pmc]
 set -eo pipefail
 TAG=${1:-r06fin}
 O=gpurun_out/$TAG
@@ -20,6 +20,7 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/rocprof_kernel_stats.csv \;
 python3 tools/rocprof_phases.py $(find $O/prof -name "*kernel_trace.csv" | head -1) $O/bench_detail_prof.json $O/rocprof_phases.json > $O/rocprof_phases.log 2>&1 || echo "phases split failed"
 echo "rocprof done"
+[ "${3:-}" = "no-pmc" ] && exit 0
 PMC_META="" bash tools/pmc.sh $O/pmc_bench --no-c4 --no-large-code --no-reference-default --no-c3 --no-cpu-baseline --steps 2
 PMC_HBM=1 PMC_META="c5_p=0.005 c5_shots=65536" bash tools/pmc_cmd.sh $O/pmc_c5_p005 tools/gpu/lines_only.py --c5 --c5-p 0.005 --c5-warm-full
 PMC_HBM=1 PMC_META="c5_p=0.001 c5_shots=65536" bash tools/pmc_cmd.sh $O/pmc_c5_p001 tools/gpu/lines_only.py --c5 --c5-p 0.001 --c5-warm-full
