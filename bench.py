@@ -271,7 +271,8 @@ def cpu_baseline(code, ps, args):
     return res
 
 
-def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005), warm_shots: int = 1 << 13):
+def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005), warm_shots: int = 1 << 13,
+                        low_p_shots: int = 1 << 18):
     """HBM roofline of the genuinely HBM-bound path: BASELINE config 5 (PSL(2,16)
     Cayley-graph LP code, n = 53,040) at R = 1 spacetime syndromes (H_st
     48,960 x 130,560, E = 236,640), BP min-sum f64 max_iter 50 + fold + logical
@@ -283,7 +284,12 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005), wa
     every shot runs all 50 iterations (LER ~1), kept as the bandwidth figure.
     The warmup launch decodes 2^13 shots (module load, scratch sizing;
     tools/gpu/lines_only.py --c5-warm-full makes it the timed launch's twin, so
-    a PMC pass's per-dispatch average is that launch's).
+    a PMC pass's per-dispatch average is that launch's).  The decoding points
+    (p <= 0.001) decode `low_p_shots` = 2^18 shots per launch: the slot-group
+    kernel keeps ~32 k slots in flight, and with 2^16 shots (two per slot) a
+    group streamed its finished slots' lines through a long tail (PMC 1.22x the
+    algorithmic bytes at p = 0.001, profiles/r06_c5_p001_pmc_summary.json);
+    the all-fail point keeps 2^16 (every shot runs 50 iterations, no tail).
     Algorithmic bytes = 32 B per edge per shot-iteration (f64 v2c read + c2v
     write in the check pass, c2v read + v2c write in the column pass) + the
     per-shot I/O (syndrome, readout, outputs)."""
@@ -305,34 +311,42 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005), wa
     sampler = Decoder(hz, 2 * ps[0] / 3, method="ms", precision="f64", max_iter=50, device=dev.index)
     dec = Decoder(H, 2 * ps[0] / 3, method="ms", precision="f64", max_iter=50, logicals=lz, n_data=nd, fold_blocks=2,
                   device=dev.index)
-    syn = torch.empty((2, shots, m), dtype=torch.uint8, device=dev)
-    rd = torch.empty((2, shots, nd), dtype=torch.uint8, device=dev)
-    iters = torch.empty((2, shots), dtype=torch.int32, device=dev)
-    status = torch.empty((2, shots), dtype=torch.uint8, device=dev)
-    fail = torch.empty((2, shots), dtype=torch.uint8, device=dev)
+    top = max([shots] + [low_p_shots for p in ps if p <= 0.001])
+    wmax = min(top, warm_shots)
+    # warmup rows [0, wmax), timed rows [wmax, wmax + top)
+    syn = torch.empty((wmax + top, m), dtype=torch.uint8, device=dev)
+    rd = torch.empty((wmax + top, nd), dtype=torch.uint8, device=dev)
+    iters = torch.empty(wmax + top, dtype=torch.int32, device=dev)
+    status = torch.empty(wmax + top, dtype=torch.uint8, device=dev)
+    fail = torch.empty(wmax + top, dtype=torch.uint8, device=dev)
     kernel = "qdec::bp_group_kernel<double, 1, 8, 4>"
     lines = []
+    full = shots
     for p in ps:
-        dec.set_priors(np.full(n, 2 * p / 3))
-        for b in range(2):
-            sampler.sample_storage_device(1, p, p, SEED, 100, b * shots, shots, syn[b], rd[b])
+        shots = low_p_shots if p <= 0.001 else full
         warm = min(shots, warm_shots)
-        dec.decode_device(warm, syn=syn[0], readout=rd[0], iters=iters[0], status=status[0], fail=fail[0])
+        dec.set_priors(np.full(n, 2 * p / 3))
+        sampler.sample_storage_device(1, p, p, SEED, 100, 0, warm, syn[:warm], rd[:warm])
+        sampler.sample_storage_device(1, p, p, SEED, 100, top, shots, syn[wmax:wmax + shots], rd[wmax:wmax + shots])
+        dec.decode_device(warm, syn=syn[:warm], readout=rd[:warm], iters=iters[:warm], status=status[:warm],
+                          fail=fail[:warm])
         torch.cuda.synchronize(dev)
         dec.set_timing(1)
         t0 = time.perf_counter()
-        dec.decode_device(shots, syn=syn[1], readout=rd[1], iters=iters[1], status=status[1], fail=fail[1])
+        T = slice(wmax, wmax + shots)
+        dec.decode_device(shots, syn=syn[T], readout=rd[T], iters=iters[T], status=status[T], fail=fail[T])
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         bp_ms, _ = dec.read_timing()
         kernel = dec.last_kernels()[0] or kernel
-        it_sum = int(iters[1].to(torch.int64).sum().item())
+        it_sum = int(iters[T].to(torch.int64).sum().item())
         io = shots * (m + nd + 1 + 1 + 4)
         algo = 32 * E * it_sum + io
         achieved = algo / (float(bp_ms[0]) * 1e-3) / 1e9
-        row = {"p": p, "shots_per_s": shots / wall, "bp_kernel_ms": float(bp_ms[0]), "mean_bp_iters": it_sum / shots,
-               "bp_converged_frac": float((status[1] & 1).to(torch.float64).mean().item()),
-               "ler": float(fail[1].to(torch.float64).mean().item()),
+        row = {"p": p, "shots": shots, "shots_per_s": shots / wall, "bp_kernel_ms": float(bp_ms[0]),
+               "mean_bp_iters": it_sum / shots,
+               "bp_converged_frac": float((status[T] & 1).to(torch.float64).mean().item()),
+               "ler": float(fail[T].to(torch.float64).mean().item()),
                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": algo}}
         pmc = pmc_ceilings(kernel, c5_p=p, c5_shots=shots)  # PMC passes of exactly this launch shape
@@ -344,7 +358,8 @@ def large_code_roofline(dev, shots: int = 1 << 16, ps=(0.0005, 0.001, 0.005), wa
         lines.append(row)
     res = {"config": "C5 as named: PSL(2,16) Cayley-graph LP (lifted_product_code_pgl2(1,4,2,double_cover=False,"
                      "seed=1)), n=53040 k=4080, R=1 spacetime 48960x130560 E=236640, BP min-sum f64 max_iter 50, "
-                     f"fold + logical check, {shots} device-sampled shots per launch",
+                     f"fold + logical check, device-sampled, {low_p_shots} shots per launch at p <= 0.001, "
+                     f"{full} above",
            "kernel": kernel,
            "bytes_model": "32 B per edge per shot-iteration (f64 messages: v2c read + c2v write, c2v read + v2c "
                           "write) + per-shot I/O",

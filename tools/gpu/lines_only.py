@@ -31,9 +31,9 @@ if args.c3:
         print("c3", ln["p"], f"{ln['shots_per_s']:.4g} shots/s", f"triage {ln['triage_ms']:.3f} bp {ln['bp_kernel_ms']:.3f} "
               f"ssf {ln['ssf_kernel_ms']:.3f} ms", f"frac {ln['roofline']['frac']:.3f}", f"ler {ln['ler']:.3g}")
 if args.c5:
-    kw = {"shots": args.shots} if args.shots else {}
-    if args.c5_warm_full:
-        kw["warm_shots"] = args.shots or (1 << 16)
+    kw = {"shots": args.shots, "low_p_shots": args.shots} if args.shots else {}
+    if args.c5_warm_full:  # the warmup launch as large as the timed one (one launch shape per PMC pass)
+        kw["warm_shots"] = 1 << 30
     res["c5"] = bench.large_code_roofline(dev, ps=tuple(args.c5_p or (0.0005, 0.001, 0.005)), **kw)
     for ln in res["c5"]["lines"]:
         print("c5", ln["p"], f"{ln['shots_per_s']:.4g} shots/s", f"bp {ln['bp_kernel_ms']:.1f} ms",
