@@ -1647,7 +1647,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                         const uint32_t sg = ((pw >> (i & 31)) ^ (uint32_t)((vb - 1ull) >> 63)) & 1u;
                         c[k] = __longlong_as_double((long long)(dbits(y) ^ ((unsigned long long)sg << 63)));
                     }
-                    __builtin_amdgcn_sched_barrier(0);  // one edge's state in flight (registers)
+                    __builtin_amdgcn_sched_barrier(0);  // one edge's state in flight (registers; issuing a
+                                                        // column's reads together measured the same, profiles/r06ab)
                 }
                 // ldpc's order: prefix sums from the prior, then each outgoing
                 // message = prefix + (sum of the later edges, accumulated from the end)
