@@ -1,5 +1,5 @@
 """Dev: timeline of one overlapped headline step from a rocprofv3 kernel trace
-of bench.py (tools/dev/gpu_timeline.sh).  Prints each BP / SSF kernel's start,
+of bench.py (a rocprofv3 --kernel-trace run of bench.py; its round-3 launcher was removed in round 6).  Prints each BP / SSF kernel's start,
 end and queue relative to the step's first start."""
 import csv, sys
 from collections import defaultdict
