@@ -780,10 +780,23 @@ LINE_MAX_BYTES = 8000  # the driver's parser; round 5's 20 KB line was not read 
 
 
 def _r(x, nd: int = 4):
-    """Round a float to `nd` significant digits for the compact line."""
+    """Round a float to `nd` significant digits for the compact line (None for
+    a non-finite value: the line must stay strict JSON)."""
     if x is None or isinstance(x, (bool, int, str)):
         return x
-    return float(f"{float(x):.{nd}g}")
+    x = float(x)
+    return float(f"{x:.{nd}g}") if math.isfinite(x) else None
+
+
+def _finite(o):
+    """Non-finite floats anywhere in a record -> None (strict JSON)."""
+    if isinstance(o, float):
+        return o if math.isfinite(o) else None
+    if isinstance(o, dict):
+        return {k: _finite(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_finite(v) for v in o]
+    return o
 
 
 def compact_line(full: dict, detail: str) -> dict:
@@ -1152,12 +1165,12 @@ def main():
         try:
             os.makedirs(os.path.dirname(detail), exist_ok=True)
             with open(detail, "w") as fh:
-                json.dump(result, fh, indent=1)
+                json.dump(_finite(result), fh, indent=1, allow_nan=False)
         except OSError as e:  # the line still goes out; it says where the detail is not
             detail = f"unwritten ({e})"
         if os.path.isabs(detail) and detail.startswith(REPO + os.sep):
             detail = os.path.relpath(detail, REPO)
-        print(json.dumps(compact_line(result, detail)))
+        print(json.dumps(_finite(compact_line(result, detail)), allow_nan=False))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -96,7 +96,10 @@ def test_compact_line_bound_with_every_config_block(tmp_path):
         row["cpu_f64"] = {"failures": 10 ** 6, "shots": 10 ** 7}
         row["f32"] = {"failures": 10 ** 6}
     full["ranks"] = full["ranks"] * 8
-    line = json.dumps(bench.compact_line(full, "gpurun_out/bench_detail.json"))
+    full["roofline"]["frac"] = float("nan")  # a non-finite value never reaches the line
+    full["value"] = float("inf")
+    line = json.dumps(bench._finite(bench.compact_line(full, "gpurun_out/bench_detail.json")), allow_nan=False)
     assert len(line) < bench.LINE_MAX_BYTES, len(line)
     r = json.loads(line)
     assert set(r["configs"]) == {"c3", "c4_f32", "c4_f64", "c5", "reference_default"}
+    assert r["roofline"]["frac"] is None and r["value"] is None
