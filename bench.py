@@ -685,6 +685,12 @@ class Run:
             self.streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
             if args.schedule == "pipeline":
                 self.ssf_stream = torch.cuda.Stream(dev)
+        # --ssf-streams: every point's SSF kernels on a stream of their own
+        # (qd_graph_set_ssf_stream; the handle's two SSF queues let its next BP
+        # stage run while this SSF kernel waits for a CU)
+        self.ssf_streams = None
+        if not fake and args.ssf_streams and args.schedule == "streams":
+            self.ssf_streams = [torch.cuda.Stream(dev) for _ in ps]
 
     def shot0(self, s):
         return (s * self.world + self.rank) * self.B
@@ -702,8 +708,14 @@ class Run:
         barrier()  # sharding: CPU word over the gloo bookkeeping group
 
     def pipelined(self, decs, on: bool):
-        """Route (or stop routing) the decoders' SSF kernels to the SSF stream."""
-        if self.fake or self.ssf_stream is None:
+        """Route (or stop routing) the decoders' SSF kernels to the SSF stream(s)."""
+        if self.fake:
+            return
+        if self.ssf_streams is not None:
+            for d, st in zip(decs, self.ssf_streams):
+                d.set_ssf_stream(st if on else None)
+            return
+        if self.ssf_stream is None:
             return
         for d in decs:
             d.set_ssf_stream(self.ssf_stream if on else None)
@@ -935,6 +947,9 @@ def main():
                          "and roofline, every config line; the stdout line names it")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 line (c3_line; rank 0, N=1 only)")
     ap.add_argument("--fake-device", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--ssf-streams", type=int, default=0, choices=[0, 1],
+                    help="streams schedule: 1 = every point's SSF kernels on their own stream (split SSF, "
+                         "double-buffered queues), 0 = on the point's stream behind its BP kernel")
     ap.add_argument("--ssf-fuse", type=int, default=0, choices=[0, 1],
                     help="1: SSF inside the compact BP kernel (QD_OPT_SSF_FUSE); 0: queue + ssf_lut_kernel")
     # diagnostic: decode without SSF (prices SSF inside the overlapped step)
@@ -1129,7 +1144,8 @@ def main():
                        "parallelism": f"shot-sharded x{world}, no collective",
                        "inputs": "bit-packed u64 rows (QD_INPUT_PACKED)" if args.inputs == "packed" else "byte rows",
                        "schedule": args.schedule if args.schedule == "pipeline" else
-                       f"{args.streams} streams, joined {'every step' if args.step_join == 'step' else 'at the end'}",
+                       f"{args.streams} streams, joined {'every step' if args.step_join == 'step' else 'at the end'}"
+                       + (", SSF on a stream per point" if args.ssf_streams else ""),
                        "wave_waves_per_cu": {k: (v or "default") for k, v in occ.items()}},
         }
         if variant:

@@ -133,6 +133,16 @@ struct qd_graph {
     // stream behind ssf_ev (nullptr: the decode's own stream)
     hipStream_t ssf_stream = nullptr;
     hipEvent_t ssf_ev = nullptr;
+    // split-SSF decodes alternate between two SSF queues (queue 1: qws2, the
+    // SSF region of the layout; control words ctl + 32 * q), so a decode waits
+    // for the SSF kernel of the decode two back on this handle, not the last
+    // one: ssf_done[q] is recorded on the SSF stream behind the kernel that
+    // used queue q
+    void* qws2 = nullptr;
+    int64_t q2_cap = 0;
+    int q_buf = 0;
+    hipEvent_t ssf_done[2] = {nullptr, nullptr};
+    bool ssf_done_live[2] = {false, false};
     hipStream_t ws_last = nullptr;
     // kernels the last decode on this handle launched (qd_graph_last_kernels)
     std::string last_bp, last_ssf, last_pre;
@@ -146,6 +156,7 @@ struct qd_graph {
 namespace {
 
 constexpr int kTimingEvents = 5;
+constexpr size_t kCtlBytes = 512;  // control words: queue q's at ctl + 32 q (u64), the HGP counter at 16
 
 template <typename T>
 int drs() { return lds_stride<T, kDR>(); }
@@ -168,6 +179,8 @@ void ws_release(qd_graph* G, hipStream_t s) {
 }
 void ws_drain(qd_graph* G) {
     if (G->ws_ev_live) hip_check(hipEventSynchronize(G->ws_ev), "hipEventSynchronize");
+    for (int q = 0; q < 2; ++q)
+        if (G->ssf_done_live[q]) hip_check(hipEventSynchronize(G->ssf_done[q]), "hipEventSynchronize");
 }
 
 // Layout of the compressed-state min-sum kernel (qdec_bp_ms.h).  Variable
@@ -935,6 +948,30 @@ void attach_queue(qd_graph* G, DecodeArgs& a, int method, int precision) {
     }
 }
 
+// The second SSF queue of split-SSF decodes (the SSF region of the layout:
+// count, index, entries; the compact lists stay in the first buffer, which only
+// the BP stage uses)
+void attach_queue2(qd_graph* G, DecodeArgs& a) {
+    if (!a.q_count) return;  // no queue for this launch
+    const DevGraph& g = G->dg;
+    if (G->q2_cap < G->q_cap) {
+        ws_drain(G);
+        if (G->qws2) hip_check(hipFree(G->qws2), "hipFree queue 2");
+        G->qws2 = nullptr;
+        G->q2_cap = 0;
+        const QueueLayout L = queue_layout(g, G->q_cap);
+        hip_check(hipMalloc(&G->qws2, g.wave ? L.cmp_count : L.bytes), "hipMalloc queue 2");
+        G->q2_cap = G->q_cap;
+    }
+    const QueueLayout L = queue_layout(g, G->q2_cap);
+    auto* base = static_cast<uint8_t*>(G->qws2);
+    a.q_count = reinterpret_cast<int32_t*>(base);
+    a.q_idx = reinterpret_cast<int64_t*>(base + L.idx);
+    a.q_x = base + L.x;
+    a.q_r = base + L.r;
+    a.q_w = reinterpret_cast<uint64_t*>(a.q_x);
+}
+
 // after a launch: a two-pass decode (its triage ran) used one counter set and
 // zeroed the other, so the next one takes the other set
 void flip_counters(qd_graph* G, const DecodeArgs& a) {
@@ -1077,7 +1114,7 @@ DecodeArgs make_args(const qd_graph* g, const qd_params* p, int64_t B, const uin
     a.ssf_steps = ssf_steps;
     a.fail = fail;
     if (!syn && !(a.syn_flags && (base || readout))) throw Fail(-7, "no syndrome source");
-    if (!g->ctl) hip_check(hipMalloc(&const_cast<qd_graph*>(g)->ctl, 256), "hipMalloc control block");
+    if (!g->ctl) hip_check(hipMalloc(&const_cast<qd_graph*>(g)->ctl, kCtlBytes), "hipMalloc control block");
     a.wave_ctr = static_cast<unsigned long long*>(g->ctl);
     a.ssf_nosplit = g->dg.opt_ssf == kSsfScanNoSplit ? 1 : 0;
     return a;
@@ -1302,7 +1339,7 @@ int qd_graph_hgp_decode_bp(qd_graph* G, int64_t B, const uint8_t* syn, uint8_t* 
         if (B < 0 || (B > 0 && !syn) || max_iter < 1) throw Fail(-92, "invalid HGP decode arguments");
         if (hgp_plan_load(P, G->num_cus, hgp_target_arch(G->device).c_str()) != 0)
             throw Fail(-93, "HGP kernel load failed");
-        if (!G->ctl) hip_check(hipMalloc(&G->ctl, 256), "hipMalloc control block");
+        if (!G->ctl) hip_check(hipMalloc(&G->ctl, kCtlBytes), "hipMalloc control block");
         if (B == 0) return;
         HgpBpArgs a{};
         a.syn = syn;
@@ -1336,6 +1373,14 @@ int qd_graph_destroy(qd_graph* g) {
         (void)hipSetDevice(g->device);
         if (g->stream) (void)hipStreamSynchronize(g->stream);
         if (g->ws_ev_live) (void)hipEventSynchronize(g->ws_ev);
+        for (int q = 0; q < 2; ++q)
+            if (g->ssf_done[q]) {
+                if (g->ssf_done_live[q]) (void)hipEventSynchronize(g->ssf_done[q]);
+                (void)hipEventDestroy(g->ssf_done[q]);
+                g->ssf_done[q] = nullptr;
+                g->ssf_done_live[q] = false;
+            }
+        if (g->qws2) (void)hipFree(g->qws2);
         if (g->ws_ev) (void)hipEventDestroy(g->ws_ev);
         g->ws_ev = nullptr;
         g->ws_ev_live = false;  // drained above (free_timing's drain is a no-op)
@@ -1765,19 +1810,32 @@ int qd_decode_batch_device(qd_graph* G, const qd_params* p, int64_t B, const uin
         void* scr = message_scratch(G, p->method, p->precision, a, &sb);
         const hipStream_t s = (hipStream_t)stream;
         const bool split = G->ssf_stream && G->ssf_stream != s && a.ssf;
+        const int qb = split ? G->q_buf : 0;
         if (split) {
             a.ssf_stream = G->ssf_stream;
             a.ssf_ev = G->ssf_ev;
+            if (qb == 1) attach_queue2(G, a);
+            a.wave_ctr = static_cast<unsigned long long*>(G->ctl) + 32 * qb;
         }
         ws_acquire(G, s);
+        // the SSF kernel that last used this decode's queue (split decodes: two
+        // back on this handle) must have finished before the queue is reset
+        if (G->ssf_done_live[qb]) hip_check(hipStreamWaitEvent(s, G->ssf_done[qb], 0), "hipStreamWaitEvent");
         const int rc = launch_decode(G->dg, p->method, p->precision, a, G->num_cus, s, scr, sb);
         note_kernels(G);
         flip_counters(G, a);  // also after a failed BP launch: its triage zeroed the other set
         if (rc != 0) throw Fail(-101, std::string("decode launch failed: ") + hipGetErrorString((hipError_t)rc));
-        note_listed(G, a, s, split ? G->ssf_stream : s);
-        // the last user of the queue is the SSF kernel: the workspace chain
-        // continues on its stream (the next decode on this handle waits for it)
-        ws_release(G, split ? G->ssf_stream : s);
+        note_listed(G, a, s, s);
+        if (split) {  // the SSF kernel runs on its own stream behind this decode's BP
+            if (!G->ssf_done[qb])
+                hip_check(hipEventCreateWithFlags(&G->ssf_done[qb], hipEventDisableTiming), "hipEventCreate");
+            hip_check(hipEventRecord(G->ssf_done[qb], G->ssf_stream), "hipEventRecord");
+            G->ssf_done_live[qb] = true;
+            G->q_buf ^= 1;
+        }
+        // the workspace chain (message scratch, compact lists, counters) ends with
+        // the BP stage; the SSF queues are ordered by ssf_done
+        ws_release(G, s);
     });
 }
 

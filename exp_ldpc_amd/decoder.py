@@ -315,9 +315,9 @@ class Decoder:
         """Run the SSF kernel of later decode_device calls on `stream` (a torch
         stream or a raw hipStream_t; None = the decode's own stream); see
         qd_graph_set_ssf_stream: the caller synchronises with that stream.
-        The handle's workspace is single-buffered, so this handle's next
-        decode still waits for the SSF kernel: overlap happens only across
-        handles (e.g. one Decoder per p point)."""
+        Split decodes alternate between two SSF queues, so this handle's next
+        decode (triage + BP) overlaps this one's SSF kernel; the one after it
+        waits for it."""
         raw = None if stream is None else int(getattr(stream, "cuda_stream", stream))
         _abi.check(self._lib.qd_graph_set_ssf_stream(self._handle, C.c_void_p(raw)), "qd_graph_set_ssf_stream")
 

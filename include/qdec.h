@@ -196,11 +196,11 @@ int qd_graph_set_timing(qd_graph* g, int32_t capacity);
  * it runs behind an event recorded after the BP kernel on the decode stream.
  * Outputs the SSF stage writes (status, ssf_steps, fail, x/corr of BP-failed
  * shots) are complete when `ssf_stream` has passed that point; the caller
- * synchronises with it.  The handle's SSF queue and control block are single-
- * buffered, so the handle's next decode waits for this SSF kernel (workspace
- * chain): on ONE handle a following BP launch never overlaps the previous SSF;
- * overlap is only possible between decodes on different handles.  Replaces
- * nothing in the reference (its decode is one synchronous call per shot). */
+ * synchronises with it.  Split decodes alternate between two SSF queues (and
+ * their control words), so a decode waits for the SSF kernel of the decode two
+ * back on this handle, not the previous one: the handle's next triage and BP
+ * run while this SSF kernel is still on `ssf_stream`.  Replaces nothing in the
+ * reference (its decode is one synchronous call per shot). */
 int qd_graph_set_ssf_stream(qd_graph* g, void* ssf_stream);
 
 /* Occupancy of the wave BP kernels (one wave per shot, persistent grid) in waves

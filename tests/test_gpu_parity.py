@@ -314,6 +314,43 @@ def test_kernel_timing_ring(gpu_available, oracle_lib, code225):
     dec.decode(syn, readout=rd, want=("fail",))
 
 
+@pytest.mark.parametrize("packed", [False, True])
+def test_split_ssf_back_to_back_on_one_handle(gpu_available, oracle_lib, packed):
+    """Split SSF (qd_graph_set_ssf_stream) with its double-buffered queues: five
+    decodes on ONE handle enqueued back to back on one BP stream, their SSF
+    kernels on a second stream (decode k's BP overlaps decode k-1's SSF; decode
+    k waits only for decode k-2's SSF).  Every output equals the oracle."""
+    import torch
+    from exp_ldpc_amd.decoder import Decoder, pack_rows
+    dev = torch.device("cuda", 0)
+    p, B, K = 0.06, 4096, 5
+    lz = np.asarray(load_code("hgp_12_3_4_s1234").logicals.z) % 2
+    syn, rd = oracle_lib.sample_storage(HZ, 0, p, p, seed=21, stream=1, shot0=0, B=K * B)
+    ref = oracle_lib.decode(HZ, 2 * p / 3, syn, method="ms", precision="f64", max_iter=50, ssf=True, gens=HX,
+                            lz=lz, readout=rd, want_llr=False, ssf_impl="fast")
+    dec = Decoder(HZ, 2 * p / 3, method="ms", precision="f64", max_iter=50, flip_sets=HX, logicals=lz)
+    if packed:
+        syn_d = torch.from_numpy(pack_rows(syn).view(np.int64)).to(dev)
+        rd_d = torch.from_numpy(pack_rows(rd).view(np.int64)).to(dev)
+    else:
+        syn_d, rd_d = torch.from_numpy(syn).to(dev), torch.from_numpy(rd).to(dev)
+    outs = {k: torch.full((K * B,), 7, dtype=dt, device=dev) for k, dt in
+            (("iters", torch.int32), ("status", torch.uint8), ("ssf_steps", torch.int32), ("fail", torch.uint8))}
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    dec.set_ssf_stream(s2)
+    for k in range(K):
+        sl = slice(k * B, (k + 1) * B)
+        dec.decode_device(B, syn=syn_d[sl], readout=rd_d[sl], stream=s1.cuda_stream, packed=packed,
+                          **{n: v[sl] for n, v in outs.items()})
+    torch.cuda.synchronize()
+    dec.set_ssf_stream(None)
+    assert dec.last_kernels()[1]  # an SSF kernel ran
+    for n, v in outs.items():
+        assert np.array_equal(v.cpu().numpy(), ref[n]), n
+    assert ref["ssf_steps"].sum() > 0
+
+
 def test_ssf_stream_split_and_handle_chain(gpu_available, oracle_lib):
     """qd_graph_set_ssf_stream: BP on one stream, SSF on another behind an event;
     then two decodes on ONE handle enqueued on two different streams back to back
