@@ -20,6 +20,10 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/rocprof_kernel_stats.csv \;
 python3 tools/rocprof_phases.py $(find $O/prof -name "*kernel_trace.csv" | head -1) $O/bench_detail_prof.json $O/rocprof_phases.json > $O/rocprof_phases.log 2>&1 || echo "phases split failed"
 echo "rocprof done"
+# two ranks on the one GPU (rank r uses device r mod visible devices): the N > 1
+# launch path and its one JSON line (not a scaling figure)
+timeout -k 10 400 python -u bench.py --gpus 2 --no-cpu-baseline --detail-out $O/bench_2ranks_detail.json > $O/bench_2ranks.json 2> $O/bench_2ranks.err
+python -c "import json; d=json.load(open('$O/bench_2ranks.json')); print('2 ranks:', d['n_gpus'], d['value']/1e6, 'M/s', d['ranks_seen'])"
 [ "${3:-}" = "no-pmc" ] && exit 0
 PMC_META="" bash tools/pmc.sh $O/pmc_bench --no-c4 --no-large-code --no-reference-default --no-c3 --no-cpu-baseline --steps 2
 PMC_HBM=1 PMC_META="c5_p=0.005 c5_shots=65536" bash tools/pmc_cmd.sh $O/pmc_c5_p005 tools/gpu/lines_only.py --c5 --c5-p 0.005 --c5-warm-full
