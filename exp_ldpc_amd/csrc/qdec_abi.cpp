@@ -211,6 +211,7 @@ void m64_layout(qd_graph* G, int m, int n, const std::vector<int32_t>& rp, const
     struct Entry {
         std::vector<int32_t> rp, ci;
         std::vector<uint16_t> et, chk;
+        int d3r;
     };
     static std::mutex mu;
     static std::vector<Entry> cache;
@@ -220,6 +221,7 @@ void m64_layout(qd_graph* G, int m, int n, const std::vector<int32_t>& rp, const
             if (c.rp == rp && c.ci == ci) {
                 g.m64_etab = G->arena.upload(c.et);
                 g.m64_check = G->arena.upload(c.chk);
+                g.m64_d3r = c.d3r;
                 return;
             }
     }
@@ -288,12 +290,21 @@ void m64_layout(qd_graph* G, int m, int n, const std::vector<int32_t>& rp, const
             move(i, sj, si);
         }
     }
-    Entry e{rp, ci, std::vector<uint16_t>((size_t)kMlDC * n, 0xffff), std::vector<uint16_t>(m)};
+    // leading rounds whose columns all have degree <= 3 (the kernel's D3R)
+    int d3r = 0;
+    while (d3r < rounds) {
+        bool ok = true;
+        for (int j = d3r * T; j < std::min(n, (d3r + 1) * T) && ok; ++j) ok = colchk[(size_t)(kMlDC - 1) * n + j] < 0;
+        if (!ok) break;
+        ++d3r;
+    }
+    Entry e{rp, ci, std::vector<uint16_t>((size_t)kMlDC * n, 0xffff), std::vector<uint16_t>(m), d3r};
     for (size_t t = 0; t < colchk.size(); ++t)
         if (colchk[t] >= 0) e.et[t] = (uint16_t)slot[colchk[t]];
     for (int i = 0; i < m; ++i) e.chk[slot[i]] = (uint16_t)i;
     g.m64_etab = G->arena.upload(e.et);
     g.m64_check = G->arena.upload(e.chk);
+    g.m64_d3r = d3r;
     std::lock_guard<std::mutex> lk(mu);
     if (cache.size() >= 8) cache.erase(cache.begin());
     cache.push_back(std::move(e));
@@ -813,6 +824,7 @@ void build_tables(qd_graph* G, int m, int n) {
         g.ml_etab = nullptr;
         g.m64_etab = nullptr;
         g.m64_check = nullptr;
+        g.m64_d3r = 0;
         if (g.max_rdeg <= kMlDRS && g.max_cdeg <= kMlDC && (size_t)m * kMlDRS + 64 < 0xffff) {
             const std::vector<int> pos = ml_positions(m, n, rp, ci, edge_cpos);
             std::vector<uint16_t> et((size_t)kMlDC * n, 0xffff);

@@ -1443,26 +1443,34 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
 //   m1[b][i], m2[b][i]  u64 bits (two arrays): minimum and second minimum of
 //             |v| over the row, with multiplicity (a repeated minimum gives m2 = m1)
 //   parw[b]   per check: syndrome ^ parity of (v <= 0) over the row
-//   tiew[b]   per check: "an edge with |v| == m1 was seen" (the second such edge
-//             sets m2 = m1)
 //   hdw[b]    per check: parity of the hard decision (the syndrome test)
+// Both minima come from ONE pass of the messages: each message x does
+//   old = ds_min_rtn_u64(m1, x);  ds_min_u64(m2, max(old, x)).
+// The updates of m1 are atomic, so they have a total order; with a1 <= a2 <= ...
+// the row's sorted values, min over the messages of max(old, x) is a2:
+//   >= a2: a message x >= a2 gives max >= a2; a minimum message x = a1 whose old
+//          is >= a2 too unless an equal minimum came first (then a2 = a1);
+//   <= a2: of the messages holding a1 and a2, the later one sees old <= the
+//          other's value, and its max is a2.
+// so m2 is the second minimum with multiplicity (kBig for a row of one edge),
+// the two-pass construction's value bit for bit, without the second pass over
+// the messages and its barrier.
 // Buffers alternate by iteration parity b = it & 1.  Per iteration (2 barriers):
 //   D  variable pass: c2v of edge (i, v) = alpha * (|v| == m1 ? m2 : m1) with
 //      sign parw ^ (v <= 0) -- ldpc's leave-one-out minimum and sign, the same
 //      selection as MsCore's and the f32 kernel's -- then ldpc's prefix / suffix
 //      sums, the hard decision (xor into hdw[b]), and the new v2c messages'
-//      atomics into buffer b ^ 1: ds_min_u64 on m1, xor of the sign parity
-//   B  syndrome test of hdw[b] (a flag per wave); second pass of the new
-//      messages on buffer b ^ 1 (|v| == m1: claim the tie bit, a second claimer
-//      sets m2 = m1; |v| > m1: ds_min_u64 on m2); buffer b reset for
-//      iteration it + 2 (every read of it is behind the barrier)
+//      atomics into buffer b ^ 1 (the two minima above, xor of the sign parity)
+//   B  syndrome test of hdw[b] (a flag per wave); buffer b reset for iteration
+//      it + 2 (every read of it is behind the barrier)
 // A v2c message is never -0 (see bp_ms_lds_kernel), so (bits(v) - 1) >> 63 is
 // ldpc's (v <= 0).  Finished shots are queued like bp_ms_lds_kernel's.
 constexpr int kM64Threads = 1024;
+constexpr int kM64Nch = 5;  // check rounds per thread: 32 B of state per check in 160 KB
 
 __host__ __device__ inline size_t m64_words(const DevGraph& g) { return ((size_t)g.m + 31) / 32; }
 __host__ __device__ inline size_t m64_lds_bytes(const DevGraph& g) {
-    return kCtrl + (size_t)2 * g.m * 16 + 7 * 4 * m64_words(g) + 2 * 4 * (kM64Threads / 64);
+    return kCtrl + (size_t)2 * g.m * 16 + 5 * 4 * m64_words(g) + 2 * 4 * (kM64Threads / 64);
 }
 
 __device__ __forceinline__ unsigned long long dbits(double x) { return (unsigned long long)__double_as_longlong(x); }
@@ -1471,12 +1479,14 @@ __device__ __forceinline__ unsigned long long dbits(double x) { return (unsigned
 // m64_layout in qdec_abi.cpp: a wave's state accesses spread over the LDS
 // banks); every array below is indexed by slot, and the syndrome input and the
 // residual output go through cslot (slot -> check).
-template <int VPT>
+// D3R: the variable rounds r < D3R hold columns of degree <= 3 only (host:
+// DevGraph::m64_d3r), so their messages take 3 registers instead of kMlDC.
+template <int VPT, int D3R>
 __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, DecodeArgs a,
                                                                  const uint16_t* __restrict__ etab,
                                                                  const double* __restrict__ prior,
                                                                  const uint16_t* __restrict__ cslot) {
-    static_assert(VPT * 3 <= 32 && VPT <= 32, "degree and decision bits");
+    static_assert(VPT * 3 <= 32 && VPT <= 32 && D3R <= VPT, "degree and decision bits");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     long long* next = reinterpret_cast<long long*>(smem + 56);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1484,9 +1494,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     const int W = (int)m64_words(g);
     unsigned long long* st = reinterpret_cast<unsigned long long*>(smem + kCtrl);  // m1 [2][m], then m2 [2][m]
     uint32_t* synw = reinterpret_cast<uint32_t*>(smem + kCtrl + (size_t)2 * m * 16);
-    uint32_t* parw = synw + W;      // [2][W]
-    uint32_t* tiew = parw + 2 * W;  // [2][W]
-    uint32_t* hdw = tiew + 2 * W;   // [2][W]
+    uint32_t* parw = synw + W;     // [2][W]
+    uint32_t* hdw = parw + 2 * W;  // [2][W]
     int* flags = reinterpret_cast<int*>(hdw + 2 * W);  // [2][16]
     // variable slot of this thread: tid * 67 mod 1024, so the 64 lanes of a wave own
     // columns 67 apart instead of 64 neighbours (neighbouring columns of a
@@ -1494,7 +1503,6 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     // state serialise its atomics)
     const int tq = (tid * 67) & (kM64Threads - 1);
     const int ncr = tid < m ? (m - tid + kM64Threads - 1) / kM64Threads : 0;  // checks of this thread
-    const int nch = (m + kM64Threads - 1) / kM64Threads;                     // check rounds (uniform)
     const unsigned long long kBig = dbits(Big<double>::v);
     constexpr unsigned long long kAbs = 0x7fffffffffffffffull;
     if (blockIdx.x == 0 && tid == 0) *a.q_count = (int32_t)a.B;
@@ -1504,9 +1512,17 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     // the messages
     uint32_t ep[VPT][kMlDC / 2];
     uint32_t djs = 0;  // 3 bits per owned variable: its degree (real edges come first)
-    auto prior_of = [&](const double* pr, int r) -> double {
-        const int j = r * kM64Threads + tq;
-        return j < n ? pr[j] : 0.0;
+    // prior of round r's column (a pad slot, j >= n, reads column n - 1: its value
+    // only reaches the pad's unused hard decision); tqv is an opaque copy of tq
+    // taken per pass, so the column offsets are re-derived where used instead of
+    // being held (spilled) across the loop
+    auto prior_of = [&](const double* pr, int tqv, int r) -> double {
+        return pr[min(r * kM64Threads + tqv, n - 1)];
+    };
+    auto opaque_tq = [&]() {
+        int t = tq;
+        asm volatile("" : "+v"(t));
+        return t;
     };
 #pragma unroll
     for (int r = 0; r < VPT; ++r) {
@@ -1529,6 +1545,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     }
     auto chk = [&](int r, int k) -> int { return (int)((ep[r][k >> 1] >> (16 * (k & 1))) & 0xffffu); };
     auto deg = [&](int r) -> int { return (int)((djs >> (3 * r)) & 7u); };
+    auto dmax = [](int r) -> int { return r < D3R ? kMlDC - 1 : kMlDC; };  // compile time once unrolled
     // keeps the per-edge addresses from being hoisted out of the loops (as in
     // bp_ms_lds_kernel): they are re-derived from ep where used
     auto opaque_edges = [&]() {
@@ -1540,43 +1557,34 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
     };
     // ldpc's (v <= 0) for a v2c message (never -0)
     auto neg = [](double v) -> uint32_t { return (uint32_t)((dbits(v) - 1ull) >> 63); };
-    // second pass of the messages v on buffer nb: m2 (with multiplicity) from m1
-    auto m2_pass = [&](const double (&v)[VPT][kMlDC], int nb) {
-        opaque_edges();
-#pragma unroll
-        for (int r = 0; r < VPT; ++r) {
-            const int dj = deg(r);
-#pragma unroll
-            for (int k = 0; k < kMlDC; ++k) {
-                if (k < dj) {
-                    const int i = chk(r, k);
-                    unsigned long long* s = st + (size_t)nb * m + i;  // m1; m2 at s + 2m
-                    const unsigned long long m1 = s[0];
-                    const unsigned long long ab = dbits(v[r][k]) & kAbs;
-                    if (ab == m1) {
-                        const uint32_t bit = 1u << (i & 31);
-                        if (atomicOr(&tiew[nb * W + (i >> 5)], bit) & bit) atomicMin(s + 2 * (size_t)m, m1);
-                    } else {
-                        atomicMin(s + 2 * (size_t)m, ab);
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
+    // one new message (magnitude bits x) into the minima of check slot i, buffer nb
+    auto put_min = [&](int nb, int i, unsigned long long x) {
+        const unsigned long long old = atomicMin(st + (size_t)nb * m + i, x);
+        atomicMin(st + (size_t)(2 + nb) * m + i, old > x ? old : x);
     };
 
+    if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
     for (;;) {
-        if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
         __syncthreads();
-        const int64_t shot = *next;
+        const long long sl = *next;  // uniform: held in SGPRs
+        const int64_t shot = (int64_t)((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)sl) |
+                                       ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(sl >> 32)) << 32));
         if (shot >= a.B) break;
-        // ---- S: syndrome words (ballots of 64 consecutive slots), both buffers reset
-        uint32_t sb = 0;  // syndrome bits of the owned slots
-        for (int c = 0; c < nch; ++c) {
+        // the next shot's index, fetched under this shot's syndrome loads (stored
+        // behind the barrier below, after every thread has read this one)
+        long long shot_next = 0;
+        if (tid == 0) shot_next = (long long)atomicAdd(a.wave_ctr, 1ull);
+        // ---- S: syndrome words (ballots of 64 consecutive slots), both buffers reset;
+        // the kM64Nch loads of a thread are issued together (clamped index, masked)
+        uint32_t sv[kM64Nch];
+#pragma unroll
+        for (int c = 0; c < kM64Nch; ++c) {
             const int i = c * kM64Threads + tid;
-            const uint32_t s = i < m ? (uint32_t)(a.syn[shot * m + cslot[i]] & 1) : 0u;
-            sb |= s << c;
-            const unsigned long long bw = __ballot(s != 0u);
+            sv[c] = a.syn[shot * m + cslot[min(i, m - 1)]] & (i < m ? 1u : 0u);
+        }
+#pragma unroll
+        for (int c = 0; c < kM64Nch; ++c) {
+            const unsigned long long bw = __ballot(sv[c] != 0u);
             const int w0 = (c * kM64Threads + wv * 64) >> 5;
             if (lane < 2 && w0 + lane < W) {
                 const uint32_t word = (uint32_t)(bw >> (32 * lane));
@@ -1585,36 +1593,34 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 parw[W + w0 + lane] = word;
             }
         }
-        for (int w = tid; w < W; w += kM64Threads) {
-            tiew[w] = tiew[W + w] = 0u;
-            hdw[w] = hdw[W + w] = 0u;
-        }
+        for (int w = tid; w < W; w += kM64Threads) hdw[w] = hdw[W + w] = 0u;
         for (int i = tid; i < 2 * m; i += kM64Threads) {
             st[2 * i] = kBig;
             st[2 * i + 1] = kBig;
         }
         __syncthreads();
+        if (tid == 0) *next = shot_next;
         // ---- iteration 1's check states from v2c = prior (buffer 1)
         double v[VPT][kMlDC];
         opaque_edges();
+        const int tq0 = opaque_tq();
 #pragma unroll
         for (int r = 0; r < VPT; ++r) {
             const int dj = deg(r);
-            const double Lr = prior_of(prior, r);
+            const double Lr = prior_of(prior, tq0, r);
             const unsigned long long ab = dbits(Lr) & kAbs;
             const uint32_t ng = neg(Lr);
 #pragma unroll
             for (int k = 0; k < kMlDC; ++k) {
                 v[r][k] = Lr;
-                if (k < dj) {
+                if (k < dmax(r) && k < dj) {
                     const int i = chk(r, k);
-                    atomicMin(st + (size_t)m + i, ab);
+                    put_min(1, i, ab);
                     if (ng) atomicXor(&parw[W + (i >> 5)], 1u << (i & 31));
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __syncthreads();
-        m2_pass(v, 1);
         __syncthreads();
 
         uint32_t xb = 0, bad = 0;  // hard decisions (bit r), failing owned checks (bit c)
@@ -1629,15 +1635,16 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             int pz = 0;
             asm volatile("" : "+s"(pz));  // the prior loads stay in the loop (global, not flat)
             const double* pr = prior + pz;
+            const int tqv = opaque_tq();
 #pragma unroll
             for (int r = 0; r < VPT; ++r) {
                 const int dj = deg(r);
-                const double Lr = prior_of(pr, r);
+                const double Lr = prior_of(pr, tqv, r);
                 double c[kMlDC];
 #pragma unroll
                 for (int k = 0; k < kMlDC; ++k) {
                     c[k] = 0.0;
-                    if (k < dj) {
+                    if (k < dmax(r) && k < dj) {
                         const int i = chk(r, k);
                         const unsigned long long* s = st + (size_t)b * m + i;
                         const unsigned long long m1 = s[0], m2 = s[2 * (size_t)m];
@@ -1668,10 +1675,10 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                     const double o = started ? pre[k] + suf : pre[k];
                     suf = started ? suf + c[k] : c[k];
                     started = started || k < dj;
-                    if (k < dj) {
+                    if (k < dmax(r) && k < dj) {
                         v[r][k] = o;
                         const int i = chk(r, k);
-                        atomicMin(st + (size_t)nb * m + i, dbits(o) & kAbs);
+                        put_min(nb, i, dbits(o) & kAbs);
                         if (neg(o)) atomicXor(&parw[nb * W + (i >> 5)], 1u << (i & 31));
                         if (x) atomicXor(&hdw[b * W + (i >> 5)], 1u << (i & 31));
                     }
@@ -1679,7 +1686,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
-            // ---- B: syndrome test of iteration it; m2 of the new messages; reset
+            // ---- B: syndrome test of iteration it; reset of buffer b
             bad = 0;
             for (int c = 0; c < ncr; ++c) {
                 const int i = c * kM64Threads + tid;
@@ -1687,15 +1694,12 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             }
             const unsigned long long wb = __ballot(bad != 0u);
             if (lane == 0) flags[b * (kM64Threads / 64) + wv] = wb != 0ull;
-            const bool more = it < a.max_iter;
-            if (more) m2_pass(v, nb);
             for (int i = tid; i < m; i += kM64Threads) {
                 st[(size_t)b * m + i] = kBig;
                 st[(size_t)(2 + b) * m + i] = kBig;
             }
             for (int w = tid; w < W; w += kM64Threads) {
                 parw[b * W + w] = synw[w];
-                tiew[b * W + w] = 0u;
                 hdw[nb * W + w] = 0u;
             }
             __syncthreads();
@@ -1706,7 +1710,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 conv = true;
                 break;
             }
-            if (!more) break;
+            if (it >= a.max_iter) break;
         }
         // ---- queue the shot: hard decision, residual syndrome, converged bit
 #pragma unroll
@@ -1861,7 +1865,7 @@ bool lds_kernel_applies(const DevGraph& g, int method, int precision, const Deco
     if (method != 1 || !g.ml_etab || (precision == 0 && (!g.m64_etab || !g.m64_check))) return false;
     if (!a.syn || a.syn_flags || a.llr_out || !a.wave_ctr) return false;
     if (precision == 0) {  // bp_ms_lds64_kernel (automatic: graphs whose messages would go to HBM)
-        if (g.n > 10 * kM64Threads || g.m <= 0 || g.m > 32 * kM64Threads || a.max_iter < 1) return false;
+        if (g.n > 10 * kM64Threads || g.m <= 0 || g.m > kM64Nch * kM64Threads || a.max_iter < 1) return false;
         if (m64_lds_bytes(g) > 160 * 1024 || block_placement(g, 8) == 0) return false;
         if (g.opt_lds_kernel == 0) return false;
         return g.opt_lds_kernel == 1 || block_placement(g, 8) != 3;
@@ -1901,22 +1905,22 @@ static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus,
     return rc;
 }
 
-template <int VPT>
+template <int VPT, int D3R>
 static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     const size_t lds = m64_lds_bytes(g);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bp_ms_lds64_kernel<VPT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bp_ms_lds64_kernel<VPT, D3R>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_ms_lds64_kernel<VPT>, kM64Threads, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_ms_lds64_kernel<VPT, D3R>, kM64Threads, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
     const long long grid = std::min<long long>((long long)num_cus * per_cu, a.B);
     e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);  // shot counter
     if (e != hipSuccess) return (int)e;
     record_ev(a, 0, stream);
-    QDEC_NOTE_BP("qdec::bp_ms_lds64_kernel", VPT);
-    hipLaunchKernelGGL((bp_ms_lds64_kernel<VPT>), dim3((unsigned)grid), dim3(kM64Threads), lds, stream, g, a,
+    QDEC_NOTE_BP("qdec::bp_ms_lds64_kernel", VPT, D3R);
+    hipLaunchKernelGGL((bp_ms_lds64_kernel<VPT, D3R>), dim3((unsigned)grid), dim3(kM64Threads), lds, stream, g, a,
                        g.m64_etab, reinterpret_cast<const double*>(g.prior[1][0]), g.m64_check);
     const hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
@@ -1929,10 +1933,15 @@ static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
 static int launch_lds(const DevGraph& g, int precision, const DecodeArgs& a, int num_cus, hipStream_t stream) {
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
     if (precision == 0) {
-        const int vpt = (g.n + kM64Threads - 1) / kM64Threads;
-        if (vpt <= 4) return launch_lds64_typed<4>(g, a, num_cus, stream);
-        if (vpt <= 8) return launch_lds64_typed<8>(g, a, num_cus, stream);
-        return launch_lds64_typed<10>(g, a, num_cus, stream);
+        // the largest instantiated D3R <= the graph's (leading rounds of degree <= 3)
+        const int vpt = (g.n + kM64Threads - 1) / kM64Threads, d3r = g.m64_d3r;
+        if (vpt <= 4) return launch_lds64_typed<4, 0>(g, a, num_cus, stream);
+        if (vpt <= 8)
+            return d3r >= 4 ? launch_lds64_typed<8, 4>(g, a, num_cus, stream)
+                            : launch_lds64_typed<8, 0>(g, a, num_cus, stream);
+        if (d3r >= 6) return launch_lds64_typed<10, 6>(g, a, num_cus, stream);
+        if (d3r >= 3) return launch_lds64_typed<10, 3>(g, a, num_cus, stream);
+        return launch_lds64_typed<10, 0>(g, a, num_cus, stream);
     }
     const int vpt = (g.n + kMlThreads - 1) / kMlThreads;
     if (vpt <= 4) return launch_lds_typed<4>(g, a, num_cus, stream);

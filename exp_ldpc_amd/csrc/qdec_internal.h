@@ -112,6 +112,7 @@ struct DevGraph {
     // and [m] the check held by each slot
     const uint16_t* m64_etab;
     const uint16_t* m64_check;
+    int m64_d3r;                  // leading variable rounds (1024 columns each) of degree <= 3
     // flip sets (SSF)
     int n_gen, g_pad, g_wmax;
     const uint8_t* g_w;           // [g_pad]
