@@ -1475,6 +1475,45 @@ __host__ __device__ inline size_t m64_lds_bytes(const DevGraph& g) {
 
 __device__ __forceinline__ unsigned long long dbits(double x) { return (unsigned long long)__double_as_longlong(x); }
 
+// Iteration 1's check states depend on the priors only (every v2c message of
+// column j is its prior): m64_init_kernel builds them once per launch in slot
+// order -- m1[m], m2[m] (u64 bits, the row's minimum and second minimum of
+// |prior| with multiplicity), then par[W] (u32 words: parity of (prior <= 0) over
+// the row) -- and every shot copies them into LDS instead of running the
+// message atomics.  The values are those of the atomics (same multiset).
+__host__ __device__ inline size_t m64_image_bytes(const DevGraph& g) {
+    return (size_t)g.m * 16 + 4 * ((m64_words(g) + 1) / 2 * 2);
+}
+
+__global__ __launch_bounds__(256) void m64_init_kernel(DevGraph g, const double* __restrict__ prior,
+                                                      const uint16_t* __restrict__ cslot,
+                                                      unsigned long long* __restrict__ img) {
+    const int s = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
+    const unsigned long long kBig = dbits(Big<double>::v);
+    unsigned long long m1 = kBig, m2 = kBig;
+    uint32_t par = 0;
+    if (s < g.m) {
+        const int i = cslot[s];
+        for (int e = g.row_ptr[i]; e < g.row_ptr[i + 1]; ++e) {
+            const unsigned long long pb = dbits(prior[g.col_idx[e]]);
+            const unsigned long long x = pb & 0x7fffffffffffffffull;
+            par ^= (uint32_t)((pb - 1ull) >> 63);  // (prior <= 0); a prior is never -0
+            if (x < m1) {
+                m2 = m1;
+                m1 = x;
+            } else if (x < m2) {
+                m2 = x;
+            }
+        }
+        img[s] = m1;
+        img[(size_t)g.m + s] = m2;
+    }
+    const unsigned long long bw = __ballot(par != 0u);
+    const int w0 = (s - lane) >> 5;
+    uint32_t* pw = reinterpret_cast<uint32_t*>(img + (size_t)2 * g.m);
+    if (lane < 2 && w0 + lane < (int)m64_words(g)) pw[w0 + lane] = (uint32_t)(bw >> (32 * lane));
+}
+
 // The check states live at host-placed slots (DevGraph::m64_etab / m64_check,
 // m64_layout in qdec_abi.cpp: a wave's state accesses spread over the LDS
 // banks); every array below is indexed by slot, and the syndrome input and the
@@ -1485,7 +1524,8 @@ template <int VPT, int D3R>
 __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, DecodeArgs a,
                                                                  const uint16_t* __restrict__ etab,
                                                                  const double* __restrict__ prior,
-                                                                 const uint16_t* __restrict__ cslot) {
+                                                                 const uint16_t* __restrict__ cslot,
+                                                                 const unsigned long long* __restrict__ img) {
     static_assert(VPT * 3 <= 32 && VPT <= 32 && D3R <= VPT, "degree and decision bits");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     long long* next = reinterpret_cast<long long*>(smem + 56);
@@ -1523,6 +1563,19 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
         int t = tq;
         asm volatile("" : "+v"(t));
         return t;
+    };
+    // the same for tid: the per-shot addresses (syndrome, image, queue) are
+    // re-derived each shot instead of being hoisted out of the shot loop and spilled
+    auto opaque_tid = [&]() {
+        int t = tid;
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+    // barrier ordering LDS only: global stores (the queue) stay in flight
+    auto lds_barrier = []() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     };
 #pragma unroll
     for (int r = 0; r < VPT; ++r) {
@@ -1563,65 +1616,74 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
         atomicMin(st + (size_t)(2 + nb) * m + i, old > x ? old : x);
     };
 
+    QDEC_STAMP_DECL
     if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
+    __syncthreads();
     for (;;) {
-        __syncthreads();
         const long long sl = *next;  // uniform: held in SGPRs
         const int64_t shot = (int64_t)((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)sl) |
                                        ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(sl >> 32)) << 32));
         if (shot >= a.B) break;
+        QDEC_STAMP(4);
+        QDEC_COUNT(8, 1);
         // the next shot's index, fetched under this shot's syndrome loads (stored
         // behind the barrier below, after every thread has read this one)
+        // (an opaque offset keeps the atomic optimiser, which would wait for the
+        // result right away, off this single-lane add)
         long long shot_next = 0;
-        if (tid == 0) shot_next = (long long)atomicAdd(a.wave_ctr, 1ull);
-        // ---- S: syndrome words (ballots of 64 consecutive slots), both buffers reset;
-        // the kM64Nch loads of a thread are issued together (clamped index, masked)
-        uint32_t sv[kM64Nch];
+        if (tid == 0) {
+            int z = 0;
+            asm volatile("" : "+v"(z));
+            shot_next = (long long)atomicAdd(a.wave_ctr + z, 1ull);
+        }
+        const int to = opaque_tid();
+        // ---- S: syndrome words (ballots of 64 consecutive slots); buffer 0 reset,
+        // buffer 1 = iteration 1's states (img).  The kM64Nch syndrome loads of a
+        // thread and its image loads are issued together (clamped index, masked).
+        uint32_t sv[kM64Nch], ip[kM64Nch];
+        unsigned long long i1[kM64Nch], i2[kM64Nch];
+        const uint32_t* ipar = reinterpret_cast<const uint32_t*>(img + (size_t)2 * m);
+        const int ln = to & 63, wbase = to & ~63;
 #pragma unroll
         for (int c = 0; c < kM64Nch; ++c) {
-            const int i = c * kM64Threads + tid;
-            sv[c] = a.syn[shot * m + cslot[min(i, m - 1)]] & (i < m ? 1u : 0u);
+            const int i = c * kM64Threads + to, ic = min(i, m - 1);
+            sv[c] = a.syn[shot * m + cslot[ic]] & (i < m ? 1u : 0u);
+            i1[c] = img[ic];
+            i2[c] = img[(size_t)m + ic];
+            ip[c] = ipar[min(((c * kM64Threads + wbase) >> 5) + (ln & 1), W - 1)];
         }
 #pragma unroll
         for (int c = 0; c < kM64Nch; ++c) {
+            const int i = c * kM64Threads + to;
+            if (i < m) {
+                st[i] = kBig;
+                st[(size_t)m + i] = i1[c];
+                st[(size_t)2 * m + i] = kBig;
+                st[(size_t)3 * m + i] = i2[c];
+            }
             const unsigned long long bw = __ballot(sv[c] != 0u);
-            const int w0 = (c * kM64Threads + wv * 64) >> 5;
-            if (lane < 2 && w0 + lane < W) {
-                const uint32_t word = (uint32_t)(bw >> (32 * lane));
-                synw[w0 + lane] = word;
-                parw[w0 + lane] = word;
-                parw[W + w0 + lane] = word;
+            const int w0 = (c * kM64Threads + wbase) >> 5;
+            if (ln < 2 && w0 + ln < W) {
+                const uint32_t word = (uint32_t)(bw >> (32 * ln));
+                synw[w0 + ln] = word;
+                parw[w0 + ln] = word;
+                parw[W + w0 + ln] = word ^ ip[c];
             }
         }
-        for (int w = tid; w < W; w += kM64Threads) hdw[w] = hdw[W + w] = 0u;
-        for (int i = tid; i < 2 * m; i += kM64Threads) {
-            st[2 * i] = kBig;
-            st[2 * i + 1] = kBig;
-        }
-        __syncthreads();
+        for (int w = to; w < W; w += kM64Threads) hdw[w] = hdw[W + w] = 0u;
+        lds_barrier();
+        QDEC_STAMP(0);
         if (tid == 0) *next = shot_next;
-        // ---- iteration 1's check states from v2c = prior (buffer 1)
         double v[VPT][kMlDC];
-        opaque_edges();
-        const int tq0 = opaque_tq();
+        {
+            const int tq0 = opaque_tq();
 #pragma unroll
-        for (int r = 0; r < VPT; ++r) {
-            const int dj = deg(r);
-            const double Lr = prior_of(prior, tq0, r);
-            const unsigned long long ab = dbits(Lr) & kAbs;
-            const uint32_t ng = neg(Lr);
+            for (int r = 0; r < VPT; ++r) {
+                const double Lr = prior_of(prior, tq0, r);
 #pragma unroll
-            for (int k = 0; k < kMlDC; ++k) {
-                v[r][k] = Lr;
-                if (k < dmax(r) && k < dj) {
-                    const int i = chk(r, k);
-                    put_min(1, i, ab);
-                    if (ng) atomicXor(&parw[W + (i >> 5)], 1u << (i & 31));
-                }
+                for (int k = 0; k < kMlDC; ++k) v[r][k] = Lr;
             }
-            __builtin_amdgcn_sched_barrier(0);
         }
-        __syncthreads();
 
         uint32_t xb = 0, bad = 0;  // hard decisions (bit r), failing owned checks (bit c)
         bool conv = false;
@@ -1686,6 +1748,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
+            QDEC_STAMP(1);
+            QDEC_COUNT(9, 1);
             // ---- B: syndrome test of iteration it; reset of buffer b
             bad = 0;
             for (int c = 0; c < ncr; ++c) {
@@ -1706,25 +1770,70 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
             int any_bad = 0;
 #pragma unroll
             for (int w = 0; w < kM64Threads / 64; ++w) any_bad |= flags[b * (kM64Threads / 64) + w];
+            QDEC_STAMP(2);
             if (!any_bad) {
                 conv = true;
                 break;
             }
             if (it >= a.max_iter) break;
         }
-        // ---- queue the shot: hard decision, residual syndrome, converged bit
+        // ---- queue the shot: hard decision, residual syndrome, converged bit.
+        // The bytes are staged in LDS (the state arrays are free after the last
+        // B barrier) in column / check order and leave as whole lines: written
+        // directly, the lanes' columns 67 apart and the slot-ordered checks put
+        // every lane of a store in its own line.
+        {
+            uint8_t* sx = reinterpret_cast<uint8_t*>(st);  // [n] hard decisions
+            uint8_t* sr = sx + ((n + 15) & ~15);            // [m] residual syndrome
+            const int tqs = opaque_tq(), tt = opaque_tid();
+            int ck[kM64Nch];
 #pragma unroll
-        for (int r = 0; r < VPT; ++r) {
-            const int j = r * kM64Threads + tq;
-            if (j < n) a.q_x[shot * n + j] = (uint8_t)((xb >> r) & 1);
+            for (int c = 0; c < kM64Nch; ++c) ck[c] = cslot[min(c * kM64Threads + tt, m - 1)];
+#pragma unroll
+            for (int r = 0; r < VPT; ++r) {
+                const int j = r * kM64Threads + tqs;
+                if (j < n) sx[j] = (uint8_t)((xb >> r) & 1);
+            }
+#pragma unroll
+            for (int c = 0; c < kM64Nch; ++c)
+                if (c * kM64Threads + tt < m) sr[ck[c]] = (uint8_t)((bad >> c) & 1);
+            lds_barrier();
+            auto copy_row = [&](uint8_t* dst, const uint8_t* src, int len) {
+                if ((((uintptr_t)dst | (uintptr_t)len) & 3) == 0) {
+                    for (int w = tt; w < len / 4; w += kM64Threads)
+                        reinterpret_cast<uint32_t*>(dst)[w] = reinterpret_cast<const uint32_t*>(src)[w];
+                } else {
+                    for (int j = tt; j < len; j += kM64Threads) dst[j] = src[j];
+                }
+            };
+            copy_row(a.q_x + shot * n, sx, n);
+            copy_row(a.q_r + shot * m, sr, m);
+            if (tid == 0) {
+                a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
+                if (a.iters) a.iters[shot] = conv ? it : a.max_iter;
+            }
+            lds_barrier();  // the staged bytes are read before the next shot's S phase writes
         }
-        for (int c = 0; c < ncr; ++c) a.q_r[shot * m + cslot[c * kM64Threads + tid]] = (uint8_t)((bad >> c) & 1);
-        if (tid == 0) {
-            a.q_idx[shot] = shot | ((int64_t)(conv ? 1 : 0) << 62);
-            if (a.iters) a.iters[shot] = conv ? it : a.max_iter;
-        }
+        QDEC_STAMP(3);
     }
+    QDEC_FLUSH_AT(16);
 }
+
+#ifdef QDEC_STAMPS
+// this translation unit's phase timers (qdec_stamps is per file): slots 16.. of
+// bp_ms_lds64_kernel (tools/dev/stamps_c4.py)
+extern "C" __attribute__((visibility("default"))) int qd_dev_read_stamps_block(unsigned long long* out, int n,
+                                                                              int reset) {
+    unsigned long long h[64] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(qdec_stamps), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < 64; ++i) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[64] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(qdec_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------- launcher
 template <typename K, typename P>
@@ -1906,7 +2015,8 @@ static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus,
 }
 
 template <int VPT, int D3R>
-static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream,
+                              unsigned long long* img, size_t img_bytes) {
     const size_t lds = m64_lds_bytes(g);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bp_ms_lds64_kernel<VPT, D3R>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1918,10 +2028,14 @@ static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     const long long grid = std::min<long long>((long long)num_cus * per_cu, a.B);
     e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);  // shot counter
     if (e != hipSuccess) return (int)e;
+    if (!img || img_bytes < m64_image_bytes(g)) return (int)hipErrorInvalidValue;
+    const double* prior = reinterpret_cast<const double*>(g.prior[1][0]);
+    hipLaunchKernelGGL(m64_init_kernel, dim3((unsigned)((g.m + 255) / 256)), dim3(256), 0, stream, g, prior,
+                       g.m64_check, img);
     record_ev(a, 0, stream);
     QDEC_NOTE_BP("qdec::bp_ms_lds64_kernel", VPT, D3R);
     hipLaunchKernelGGL((bp_ms_lds64_kernel<VPT, D3R>), dim3((unsigned)grid), dim3(kM64Threads), lds, stream, g, a,
-                       g.m64_etab, reinterpret_cast<const double*>(g.prior[1][0]), g.m64_check);
+                       g.m64_etab, prior, g.m64_check, img);
     const hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;
@@ -1930,18 +2044,20 @@ static int launch_lds64_typed(const DevGraph& g, const DecodeArgs& a, int num_cu
     return rc;
 }
 
-static int launch_lds(const DevGraph& g, int precision, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+static int launch_lds(const DevGraph& g, int precision, const DecodeArgs& a, int num_cus, hipStream_t stream,
+                      void* scratch, size_t scratch_bytes) {
+    unsigned long long* img = reinterpret_cast<unsigned long long*>(scratch);  // f64: iteration 1's states
     if (!a.q_count || !a.q_idx || !a.q_x || !a.q_r) return (int)hipErrorInvalidValue;
     if (precision == 0) {
         // the largest instantiated D3R <= the graph's (leading rounds of degree <= 3)
         const int vpt = (g.n + kM64Threads - 1) / kM64Threads, d3r = g.m64_d3r;
-        if (vpt <= 4) return launch_lds64_typed<4, 0>(g, a, num_cus, stream);
+        if (vpt <= 4) return launch_lds64_typed<4, 0>(g, a, num_cus, stream, img, scratch_bytes);
         if (vpt <= 8)
-            return d3r >= 4 ? launch_lds64_typed<8, 4>(g, a, num_cus, stream)
-                            : launch_lds64_typed<8, 0>(g, a, num_cus, stream);
-        if (d3r >= 6) return launch_lds64_typed<10, 6>(g, a, num_cus, stream);
-        if (d3r >= 3) return launch_lds64_typed<10, 3>(g, a, num_cus, stream);
-        return launch_lds64_typed<10, 0>(g, a, num_cus, stream);
+            return d3r >= 4 ? launch_lds64_typed<8, 4>(g, a, num_cus, stream, img, scratch_bytes)
+                            : launch_lds64_typed<8, 0>(g, a, num_cus, stream, img, scratch_bytes);
+        if (d3r >= 6) return launch_lds64_typed<10, 6>(g, a, num_cus, stream, img, scratch_bytes);
+        if (d3r >= 3) return launch_lds64_typed<10, 3>(g, a, num_cus, stream, img, scratch_bytes);
+        return launch_lds64_typed<10, 0>(g, a, num_cus, stream, img, scratch_bytes);
     }
     const int vpt = (g.n + kMlThreads - 1) / kMlThreads;
     if (vpt <= 4) return launch_lds_typed<4>(g, a, num_cus, stream);
@@ -2077,6 +2193,8 @@ size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num
                                                                   : 0;
         return kGrpHeader + (size_t)group_count(g, method, tsz, num_cus, a.B) * group_layout(g, tsz).total + fin;
     }
+    // LDS-resident kernels: f64 takes iteration 1's state image (m64_init_kernel)
+    if (lds_kernel_applies(g, method, precision, a)) return precision == 0 ? m64_image_bytes(g) : 0;
     const int placement = block_placement(g, tsz);
     if (placement == 3) return 0;
     // shot-counter header + up to 4 workgroup slices per CU (+ the SSF/finalize
@@ -2110,7 +2228,7 @@ int launch_decode_block(const DevGraph& g, int method, int precision, const Deco
         return method == 1 ? launch_group_shape<double, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_group_shape<double, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
     }
-    if (lds) return launch_lds(g, precision, a, num_cus, stream);
+    if (lds) return launch_lds(g, precision, a, num_cus, stream, scratch, scratch_bytes);
     if (precision == 1)
         return method == 1 ? launch_block_typed<float, 1>(g, a, num_cus, stream, scratch, scratch_bytes)
                            : launch_block_typed<float, 0>(g, a, num_cus, stream, scratch, scratch_bytes);
