@@ -195,14 +195,16 @@ void ws_drain(qd_graph* G) {
 // Check-state slots of bp_ms_lds64_kernel (f64, one shot per CU; qdec_bp_block.hip).
 // Its variable thread t owns columns r * 1024 + (67 t mod 1024); per (wave,
 // round r, edge k) one LDS instruction of 64 lanes reads or atomically updates
-// the state of each lane's k-th check: u64 m1 / m2 elements (ds_read_b64,
-// ds_min_u64: bank pair = slot mod 32 per 32-lane half) and bit words
-// (parw / hdw / tiew: word = slot >> 5, bank = word mod 32).  With checks in
-// their natural order a half's 32 lanes land on ~3-4 lanes per bank (the PMC
-// of round 5: 0.61 of the kernel's LDS cycles were bank conflicts).  A seeded
-// anneal over slot swaps spreads every half over the banks (objective: sum of
-// squared lanes per bank, both keys; tools/dev/c4_bank_model.py's max-per-bank
-// model on C4: 22,975 -> ~14,600 cycles, ideal 7,072).  The kernel then works in
+// the state of each lane's k-th check.  The banking gfx950 applies
+// (tools/dev/lds_atomic_probe.hip): the u64 m1 / m2 reads (ds_read_b64) in two
+// 32-lane halves, key slot mod 32; the u64 atomics (ds_min(_rtn)_u64) in four
+// 16-lane quarters, key slot mod 16; the bit words (parw / hdw: word = slot >> 5)
+// in halves, key word mod 32.  With checks in their natural order a group's
+// lanes land on ~3-4 lanes per bank.  A seeded anneal over slot swaps spreads
+// every group over its banks (objective: sum of squared lanes per bank, all
+// three keys; tools/dev/c4_bank_model2.py's max-per-bank cycles on C4: 23,102
+// natural -> 16,086, conflict-free 7,600; an anneal of the max model itself,
+// tools/dev/c4_slots_anneal2.cpp, stops at the same 16.2k).  The kernel then works in
 // slot space; m64_check maps a slot back to its check for the syndrome input and
 // the residual output.  Cached per process like ms_layout.
 void m64_layout(qd_graph* G, int m, int n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
@@ -232,41 +234,58 @@ void m64_layout(qd_graph* G, int m, int n, const std::vector<int32_t>& rp, const
     for (int i = 0; i < m; ++i)
         for (int e = rp[i]; e < rp[i + 1]; ++e)
             if (edge_cpos[e] < kMlDC) colchk[(size_t)edge_cpos[e] * n + ci[e]] = i;
-    // the halves: 32 lanes of one instruction; occurrences of each check
-    std::vector<std::vector<int>> halves;
+    // the lane groups of one instruction: 32-lane halves (ds_read_b64 of m1 / m2,
+    // key slot mod 32; b32 words, key (slot >> 5) mod 32) and 16-lane quarters
+    // (ds_min(_rtn)_u64 on m1 / m2, key slot mod 16) -- the banking measured by
+    // tools/dev/lds_atomic_probe.hip; occurrences of each check in both
+    std::vector<std::vector<int>> halves, quarters;
     const int rounds = (n + T - 1) / T;
     for (int w = 0; w < T / 64; ++w)
         for (int r = 0; r < rounds; ++r)
             for (int k = 0; k < kMlDC; ++k)
-                for (int h = 0; h < 2; ++h) {
-                    std::vector<int> hh;
-                    for (int l = 32 * h; l < 32 * h + 32; ++l) {
+                for (int q = 0; q < 4; ++q) {
+                    std::vector<int> qq;
+                    for (int l = 16 * q; l < 16 * q + 16; ++l) {
                         const int j = r * T + ((64 * w + l) * 67) % T;
-                        if (j < n && colchk[(size_t)k * n + j] >= 0) hh.push_back(colchk[(size_t)k * n + j]);
+                        if (j < n && colchk[(size_t)k * n + j] >= 0) qq.push_back(colchk[(size_t)k * n + j]);
                     }
-                    if (!hh.empty()) halves.push_back(std::move(hh));
+                    if (q & 1) {  // the half: this quarter and the one before it
+                        std::vector<int> hh(quarters.back());
+                        hh.insert(hh.end(), qq.begin(), qq.end());
+                        if (!hh.empty()) halves.push_back(std::move(hh));
+                    }
+                    quarters.push_back(std::move(qq));
                 }
-    const int nh = (int)halves.size();
-    std::vector<std::vector<int>> occ(m);
+    const int nh = (int)halves.size(), nq = (int)quarters.size();
+    std::vector<std::vector<int>> occ(m), occq(m);
     for (int h = 0; h < nh; ++h)
         for (int i : halves[h]) occ[i].push_back(h);
+    for (int q = 0; q < nq; ++q)
+        for (int i : quarters[q]) occq[i].push_back(q);
     std::vector<int> slot(m);
     for (int i = 0; i < m; ++i) slot[i] = i;
-    std::vector<int> cx((size_t)nh * 32, 0), cy((size_t)nh * 32, 0);
+    std::vector<int> cx((size_t)nh * 32, 0), cy((size_t)nh * 32, 0), cz((size_t)nq * 16, 0);
     auto X = [](int s) { return s & 31; };
     auto Y = [](int s) { return (s >> 5) & 31; };
+    auto Z = [](int s) { return s & 15; };
     for (int h = 0; h < nh; ++h)
         for (int i : halves[h]) ++cx[(size_t)h * 32 + X(slot[i])], ++cy[(size_t)h * 32 + Y(slot[i])];
-    const double WX = 5.0, WY = 1.5;  // u64 state ops outnumber the bit-word ops
+    for (int q = 0; q < nq; ++q)
+        for (int i : quarters[q]) ++cz[(size_t)q * 16 + Z(slot[i])];
+    // per edge: two u64 reads (halves), two u64 atomics (quarters), one b32 read
+    // and the occasional b32 xor (halves)
+    const double WX = 2.0, WZ = 2.0, WY = 1.5;
     auto move = [&](int i, int from, int to) {
         for (int h : occ[i]) {
             --cx[(size_t)h * 32 + X(from)], --cy[(size_t)h * 32 + Y(from)];
             ++cx[(size_t)h * 32 + X(to)], ++cy[(size_t)h * 32 + Y(to)];
         }
+        for (int q : occq[i]) --cz[(size_t)q * 16 + Z(from)], ++cz[(size_t)q * 16 + Z(to)];
     };
     auto local = [&](int i, int s) {  // check i's share of the squared loads at slot s
         double c = 0;
         for (int h : occ[i]) c += WX * (2 * cx[(size_t)h * 32 + X(s)] - 1) + WY * (2 * cy[(size_t)h * 32 + Y(s)] - 1);
+        for (int q : occq[i]) c += WZ * (2 * cz[(size_t)q * 16 + Z(s)] - 1);
         return c;
     };
     std::mt19937_64 rng(20250221);
