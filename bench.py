@@ -474,7 +474,7 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
     2^17 / 256 groups = 512 shots per group; the config itself decodes 1e7
     shots.
     f64 runs bp_ms_lds64_kernel (v2c messages in registers, check states built
-    by LDS atomics: LDS roofline, 44 B per edge + 16 B per check per
+    by LDS atomics in one pass: LDS roofline, 44 B per edge + 16 B per check per
     shot-iteration; the slot-group kernel's HBM model, 32 B per edge per
     shot-iteration + I/O, applies when a handle forces it); f32 runs the LDS-resident kernel
     (every message on chip: LDS roofline, per shot-iteration 8 B per edge -- the
@@ -525,10 +525,10 @@ def c4_line(dev, shots: int = 1 << 19, ps=(0.005, 0.01, 0.03), precisions=("f64"
             if "lds64" in kern[0]:
                 algo = (44 * E + 16 * m) * it_sum
                 roof = {"bound": "lds", "peak": LDS_PEAK_GBS,
-                        "bytes_model": "LDS: 44 B per edge + 16 B per check per shot-iteration (variable pass: 16-B "
-                                       "(m1, m2) state + parity word read, ds_min_u64 on the next m1; second pass: m1 "
-                                       "read + ds_min_u64 on m2; check state reset), the data-dependent sign / "
-                                       "decision xors not counted"}
+                        "bytes_model": "LDS: 44 B per edge + 16 B per check per shot-iteration (one pass: 16-B "
+                                       "(m1, m2) state + parity word read, ds_min_rtn_u64 on the next m1 (8 B out, "
+                                       "8 B back), ds_min_u64 on its m2; check state reset), the data-dependent "
+                                       "sign / decision xors not counted"}
             elif "group" in kern[0]:
                 algo = 32 * E * it_sum + io
                 roof = {"bound": "hbm", "peak": HBM_PEAK_GBS,

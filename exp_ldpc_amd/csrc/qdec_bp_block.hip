@@ -1717,7 +1717,8 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                         c[k] = __longlong_as_double((long long)(dbits(y) ^ ((unsigned long long)sg << 63)));
                     }
                     __builtin_amdgcn_sched_barrier(0);  // one edge's state in flight (registers; issuing a
-                                                        // column's reads together measured the same, profiles/r06ab)
+                                                        // column's reads together measured the same, profiles/r06ab,
+                                                        // profiles/r06c4/ab_edge_batch)
                 }
                 // ldpc's order: prefix sums from the prior, then each outgoing
                 // message = prefix + (sum of the later edges, accumulated from the end)
@@ -1726,7 +1727,7 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
 #pragma unroll
                 for (int k = 0; k < kMlDC; ++k) {
                     pre[k] = acc;
-                    acc = k < dj ? acc + c[k] : acc;
+                    acc = (k < dmax(r) && k < dj) ? acc + c[k] : acc;
                 }
                 const bool x = acc <= 0.0;
                 xb |= (uint32_t)x << r;
@@ -1734,13 +1735,15 @@ __global__ __launch_bounds__(kM64Threads) void bp_ms_lds64_kernel(DevGraph g, De
                 bool started = false;
 #pragma unroll
                 for (int k = kMlDC - 1; k >= 0; --k) {
+                    if (k >= dmax(r)) continue;
                     const double o = started ? pre[k] + suf : pre[k];
                     suf = started ? suf + c[k] : c[k];
                     started = started || k < dj;
-                    if (k < dmax(r) && k < dj) {
+                    if (k < dj) {
                         v[r][k] = o;
                         const int i = chk(r, k);
-                        put_min(nb, i, dbits(o) & kAbs);
+                        put_min(nb, i, dbits(o) & kAbs);  // (every ds_min_rtn of the column first, then
+                                                          // the m2 updates: spills, 11 % slower, r06c4)
                         if (neg(o)) atomicXor(&parw[nb * W + (i >> 5)], 1u << (i & 31));
                         if (x) atomicXor(&hdw[b * W + (i >> 5)], 1u << (i & 31));
                     }
