@@ -1205,6 +1205,7 @@ __global__ __launch_bounds__(64 * grp_waves<T>()) void bp_group_kernel(DevGraph 
 // same address): they read garbage that the sums mask out and write into them,
 // so the loops have no per-edge branches; only real edges xor parity.
 constexpr int kMlThreads = 1024;
+constexpr int kMlNch = 5;  // check rounds per thread: 32 B of rows per check in 160 KB
 
 constexpr int kMlDummyRows = 64 / kMlDRS;  // pad edges of lane l use element m * kMlDRS + l
 
@@ -1277,20 +1278,43 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
         rdeg |= (uint32_t)(g.row_ptr[i + 1] - g.row_ptr[i]) << (4 * c);
     }
 
+    // The next shot's index is fetched under this shot's syndrome loads and
+    // stored behind the barrier below (every thread has read this one by then);
+    // the barriers of the shot's iterations order it before the next read.  The
+    // syndrome loads of a thread are issued together (kMlNch, clamped, masked),
+    // and the barrier orders LDS only, so the last shot's queue stores stay in
+    // flight (a __syncthreads would wait for them).
+    if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
+    __syncthreads();
     for (;;) {
-        if (tid == 0) *next = (long long)atomicAdd(a.wave_ctr, 1ull);
-        __syncthreads();
-        const int64_t shot = *next;
+        const long long sl = *next;  // uniform: held in SGPRs
+        const int64_t shot = (int64_t)((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)sl) |
+                                       ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(sl >> 32)) << 32));
         if (shot >= a.B) break;
+        long long shot_next = 0;
+        if (tid == 0) {
+            int z = 0;  // opaque offset: keeps the atomic optimiser (which waits at once) off
+            asm volatile("" : "+v"(z));
+            shot_next = (long long)atomicAdd(a.wave_ctr + z, 1ull);
+        }
+        int to = tid;
+        asm volatile("" : "+v"(to));  // per-shot addresses re-derived, not hoisted and spilled
         uint32_t sb = 0;  // syndrome bits of the owned checks
-        for (int c = 0; c < ncr; ++c) sb |= (uint32_t)(a.syn[shot * m + c * kMlThreads + tid] & 1) << c;
+#pragma unroll
+        for (int c = 0; c < kMlNch; ++c) {
+            const int i = c * kMlThreads + to;
+            sb |= (uint32_t)(a.syn[shot * m + min(i, m - 1)] & (i < m ? 1u : 0u)) << c;
+        }
         // v2c = prior on every edge
         opaque_edges();
 #pragma unroll
         for (int r = 0; r < VPT; ++r)
 #pragma unroll
             for (int k = 0; k < kMlDC; ++k) rows[edge(r, k)] = L[r];
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        if (tid == 0) *next = shot_next;
 
         uint32_t xb = 0, bad = 0;  // hard decisions (bit r), failing owned checks (bit c)
         bool conv = false;
@@ -1983,7 +2007,7 @@ bool lds_kernel_applies(const DevGraph& g, int method, int precision, const Deco
         return g.opt_lds_kernel == 1 || block_placement(g, 8) != 3;
     }
     if (precision != 1) return false;
-    if (g.n > 16 * kMlThreads || g.m <= 0 || ml_lds_bytes(g) > 160 * 1024) return false;
+    if (g.n > 16 * kMlThreads || g.m <= 0 || g.m > kMlNch * kMlThreads || ml_lds_bytes(g) > 160 * 1024) return false;
     if (block_placement(g, 4) == 0) return false;  // the SSF/finalize state would not fit LDS
     if (g.opt_lds_kernel == 0) return false;
     if (g.opt_lds_kernel == 1) return true;

@@ -313,6 +313,32 @@ def test_lds64_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypa
     _decode_lds64(oracle_lib, H, probs, syn, max_iter=1)
 
 
+@pytest.mark.parametrize("n,m,n3,inst", [(8000, 4000, 4500, "<8, 4>"), (7000, 4000, 0, "<8, 0>"),
+                                          (9800, 4800, 3500, "<10, 3>"), (9300, 4900, 0, "<10, 0>")])
+def test_lds64_kernel_degree3_rounds(gpu_available, oracle_lib, n, m, n3, inst, monkeypatch):
+    """bp_ms_lds64_kernel's D3R instantiations (leading 1024-column rounds whose
+    columns all have degree <= 3 keep 3 messages in registers): columns j < n3
+    of degree 3, the rest of degree 4, so the host's count picks the
+    instantiation asserted; x / iterations / status bit-exact."""
+    from exp_ldpc_amd.codes import make_check_matrix
+    from exp_ldpc_amd.decoder import Decoder
+    monkeypatch.setitem(decoder.DEFAULT_OPTIONS, "lds_kernel", 1)
+    rng = np.random.default_rng(n)
+    rows, cnt = [[] for _ in range(m)], np.zeros(m, int)
+    for j in range(n):  # row degrees <= 8 (the kernel's check-row bound)
+        for i in rng.choice(np.flatnonzero(cnt < 8), 3 if j < n3 else 4, replace=False):
+            rows[i].append(j)
+            cnt[i] += 1
+    H = make_check_matrix([sorted(r) for r in rows], n)
+    e = (rng.random((96, n)) < 0.01).astype(np.uint8)
+    syn = ((H @ e.T).T % 2).astype(np.uint8)
+    probs = rng.uniform(0.005, 0.03, n)
+    _decode_lds64(oracle_lib, H, probs, syn, max_iter=30)
+    dec = Decoder(H, probs, method="ms", precision="f64", max_iter=30)
+    dec.decode(syn[:4], want=("x",))
+    assert dec.last_kernels()[0].startswith("qdec::bp_ms_lds64_kernel" + inst), dec.last_kernels()
+
+
 def test_lds64_kernel_zero_and_negative_priors(gpu_available, oracle_lib, monkeypatch):
     """bp_ms_lds64_kernel on exactly-zero messages (p = 0.5 columns: +0 priors,
     ties at m1 = 0, -0 c2v) and negative priors (p > 0.5)."""
