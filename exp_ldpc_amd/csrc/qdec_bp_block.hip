@@ -1216,10 +1216,84 @@ __host__ __device__ inline size_t ml_lds_bytes(const DevGraph& g) {
     return kCtrl + ((size_t)g.m + kMlDummyRows) * kMlDRS * 4 + 2 * 4 * ml_pbuf_words(g) + 2 * 4 * (kMlThreads / 64);
 }
 
+// Step A of bp_ms_lds_kernel on row i, in place (v2c slots in, c2v slots out);
+// also ml_init_check_kernel's iteration 1 on the image in HBM.
+__device__ __forceinline__ void ml_check_row(float* rows, int i, int deg, uint32_t sbit, float alpha) {
+    // the row's halves in swizzled order (so = 4 * bit 4 of the row): the 16-B
+    // reads of a 16-lane group (banks a/4 mod 64) and the 16-B writes of an
+    // 8-lane group (banks a/4 mod 32) then land in distinct 4-bank slots; loaded
+    // element u sits at row position u ^ so
+    const int so = ((i >> 4) & 1) << 2;
+    float v[kMlDRS];
+    {
+        const float4 h0 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + so);
+        const float4 h1 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + (so ^ 4));
+        v[0] = h0.x, v[1] = h0.y, v[2] = h0.z, v[3] = h0.w;
+        v[4] = h1.x, v[5] = h1.y, v[6] = h1.z, v[7] = h1.w;
+    }
+    // sign test by bits: bit 31 of bits(v) - 1 is (v <= 0) for every v but -0,
+    // and a v2c message is never -0 (the prior is not, and a sum is -0 only when
+    // both terms are)
+    float m1 = Big<float>::v, m2 = Big<float>::v;
+    int au = 0;  // element index of the argmin
+    uint32_t sx = sbit << 31;
+    uint32_t sg[kMlDRS];
+#pragma unroll
+    for (int u = 0; u < kMlDRS; ++u) {
+        const float vt = (u ^ so) < deg ? v[u] : Big<float>::v;
+        const float av = fabsf(vt);
+        au = av < m1 ? u : au;
+        m2 = med3(av, m1, m2);
+        m1 = med3(av, m1, -Big<float>::v);
+        sg[u] = (uint32_t)__float_as_int(vt) - 1u;
+        sx ^= sg[u];
+    }
+    // c2v of every position, in place of its v2c: alpha times the leave-one-out
+    // minimum (m2 at the argmin, m1 elsewhere), sign = syndrome ^ the other
+    // edges' signs = bit 31 of sx ^ sg[u]
+    const float y1 = m1 * alpha, y2 = m2 * alpha;
+    float o[kMlDRS];
+#pragma unroll
+    for (int u = 0; u < kMlDRS; ++u) {
+        const float y = u == au ? y2 : y1;
+        o[u] = __uint_as_float(__float_as_uint(y) ^ ((sg[u] ^ sx) & 0x80000000u));
+    }
+    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + so) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + (so ^ 4)) = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+// Iteration 1's c2v rows depend on the priors and, through one sign per row, on
+// the syndrome: the image (rows of `ml_lds_bytes`' layout, m x kMlDRS f32 in
+// HBM, syndrome bit 0) is built once per launch -- the priors scattered to the
+// edge slots, then step A on every row -- and each shot copies it, flipping
+// every sign of the rows whose syndrome bit is 1 (step A's sx carries that bit
+// into all of a row's signs).  The image's unused row positions are never read
+// (step A masks positions >= the degree, and pad edges use the dummy rows).
+__host__ __device__ inline size_t ml_image_bytes(const DevGraph& g) { return (size_t)g.m * kMlDRS * 4; }
+
+__global__ __launch_bounds__(256) void ml_init_scatter_kernel(DevGraph g, const uint16_t* __restrict__ etab,
+                                                             const float* __restrict__ prior, float* __restrict__ img) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= g.n) return;
+    const float L = prior[j];
+#pragma unroll
+    for (int k = 0; k < kMlDC; ++k) {
+        const uint32_t e = etab[(size_t)k * g.n + j];
+        if (e != 0xffffu) img[e] = L;
+    }
+}
+
+__global__ __launch_bounds__(256) void ml_init_check_kernel(DevGraph g, float* __restrict__ img, double ms_scaling) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= g.m) return;
+    ml_check_row(img, i, g.row_ptr[i + 1] - g.row_ptr[i], 0u, alpha_at<float>(1, ms_scaling));
+}
+
 template <int VPT>
 __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, DecodeArgs a,
                                                               const uint16_t* __restrict__ etab,
-                                                              const float* __restrict__ prior) {
+                                                              const float* __restrict__ prior,
+                                                              const float* __restrict__ img) {
     static_assert(VPT * 3 <= 64 && VPT <= 32, "degree and decision bits");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     long long* next = reinterpret_cast<long long*>(smem + 56);
@@ -1305,12 +1379,20 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
             const int i = c * kMlThreads + to;
             sb |= (uint32_t)(a.syn[shot * m + min(i, m - 1)] & (i < m ? 1u : 0u)) << c;
         }
-        // v2c = prior on every edge
-        opaque_edges();
+        // iteration 1's c2v rows: the image, signs flipped where the syndrome bit
+        // is 1; the parity bits of iteration 1 cleared
 #pragma unroll
-        for (int r = 0; r < VPT; ++r)
-#pragma unroll
-            for (int k = 0; k < kMlDC; ++k) rows[edge(r, k)] = L[r];
+        for (int c = 0; c < kMlNch; ++c) {
+            const int i = c * kMlThreads + to;
+            if (i < m) {
+                const uint32_t f = ((sb >> c) & 1u) << 31;
+                const uint4 h0 = *reinterpret_cast<const uint4*>(img + (size_t)i * kMlDRS);
+                const uint4 h1 = *reinterpret_cast<const uint4*>(img + (size_t)i * kMlDRS + 4);
+                *reinterpret_cast<uint4*>(rows + (size_t)i * kMlDRS) = make_uint4(h0.x ^ f, h0.y ^ f, h0.z ^ f, h0.w ^ f);
+                *reinterpret_cast<uint4*>(rows + (size_t)i * kMlDRS + 4) = make_uint4(h1.x ^ f, h1.y ^ f, h1.z ^ f, h1.w ^ f);
+            }
+        }
+        for (int w = to; w < npw; w += kMlThreads) pb0[pbw + w] = 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -1321,76 +1403,38 @@ __global__ __launch_bounds__(kMlThreads) void bp_ms_lds_kernel(DevGraph g, Decod
         int it = 1;
         for (;; ++it) {
             // ---- A: test of iteration it - 1, then the c2v messages of iteration it
-            const uint32_t* pprev = pb0 + ((it - 1) & 1) * pbw;
+            // (iteration 1's came from the image)
             uint32_t* pcur = pb0 + (it & 1) * pbw;
-            const bool work = it <= a.max_iter;
-            const float alpha = alpha_at<float>(it, a.ms_scaling);
-            bad = 0;
-            for (int c = 0; c < ncr; ++c) {
-                const int i = c * kMlThreads + tid;
-                if (it > 1) bad |= (((pprev[i >> 5] >> (i & 31)) ^ (sb >> c)) & 1u) << c;
-                if (work) {
-                    const int deg = c < 8 ? (int)((rdeg >> (4 * c)) & 15u) : (g.row_ptr[i + 1] - g.row_ptr[i]);
-                    // the row's halves in swizzled order (so = 4 * bit 4 of the row):
-                    // the 16-B reads of a 16-lane group (banks a/4 mod 64) and the
-                    // 16-B writes of an 8-lane group (banks a/4 mod 32) then land in
-                    // distinct 4-bank slots; loaded element u sits at row position
-                    // u ^ so
-                    const int so = ((i >> 4) & 1) << 2;
-                    float v[kMlDRS];
-                    {
-                        const float4 h0 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + so);
-                        const float4 h1 = *reinterpret_cast<const float4*>(rows + (size_t)i * kMlDRS + (so ^ 4));
-                        v[0] = h0.x, v[1] = h0.y, v[2] = h0.z, v[3] = h0.w;
-                        v[4] = h1.x, v[5] = h1.y, v[6] = h1.z, v[7] = h1.w;
+            if (it > 1) {
+                const uint32_t* pprev = pb0 + ((it - 1) & 1) * pbw;
+                const bool work = it <= a.max_iter;
+                const float alpha = alpha_at<float>(it, a.ms_scaling);
+                bad = 0;
+                for (int c = 0; c < ncr; ++c) {
+                    const int i = c * kMlThreads + tid;
+                    bad |= (((pprev[i >> 5] >> (i & 31)) ^ (sb >> c)) & 1u) << c;
+                    if (work) {
+                        const int deg = c < 8 ? (int)((rdeg >> (4 * c)) & 15u) : (g.row_ptr[i + 1] - g.row_ptr[i]);
+                        ml_check_row(rows, i, deg, (sb >> c) & 1u, alpha);
                     }
-                    // sign test by bits: bit 31 of bits(v) - 1 is (v <= 0) for every v
-                    // but -0, and a v2c message is never -0 (the prior is not, and a
-                    // sum is -0 only when both terms are)
-                    float m1 = Big<float>::v, m2 = Big<float>::v;
-                    int au = 0;  // element index of the argmin
-                    uint32_t sx = ((sb >> c) & 1u) << 31;
-                    uint32_t sg[kMlDRS];
-#pragma unroll
-                    for (int u = 0; u < kMlDRS; ++u) {
-                        const float vt = (u ^ so) < deg ? v[u] : Big<float>::v;
-                        const float av = fabsf(vt);
-                        au = av < m1 ? u : au;
-                        m2 = med3(av, m1, m2);
-                        m1 = med3(av, m1, -Big<float>::v);
-                        sg[u] = (uint32_t)__float_as_int(vt) - 1u;
-                        sx ^= sg[u];
-                    }
-                    // c2v of every position, in place of its v2c: alpha times the
-                    // leave-one-out minimum (m2 at the argmin, m1 elsewhere), sign =
-                    // syndrome ^ the other edges' signs = bit 31 of sx ^ sg[u]
-                    const float y1 = m1 * alpha, y2 = m2 * alpha;
-                    float o[kMlDRS];
-#pragma unroll
-                    for (int u = 0; u < kMlDRS; ++u) {
-                        const float y = u == au ? y2 : y1;
-                        o[u] = __uint_as_float(__float_as_uint(y) ^ ((sg[u] ^ sx) & 0x80000000u));
-                    }
-                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + so) = make_float4(o[0], o[1], o[2], o[3]);
-                    *reinterpret_cast<float4*>(rows + (size_t)i * kMlDRS + (so ^ 4)) = make_float4(o[4], o[5], o[6], o[7]);
                 }
-            }
-            if (work)
-                for (int w = tid; w < npw; w += kMlThreads) pcur[w] = 0u;
-            // block-wide "any check failing": one flag per wave, double-buffered by
-            // iteration parity so one barrier suffices
-            int* fl = flags + (it & 1) * (kMlThreads / 64);
-            const unsigned long long wb = __ballot(bad != 0u);
-            if ((tid & 63) == 0) fl[tid >> 6] = wb != 0ull;
-            __syncthreads();
-            int any_bad = 0;
+                if (work)
+                    for (int w = tid; w < npw; w += kMlThreads) pcur[w] = 0u;
+                // block-wide "any check failing": one flag per wave, double-buffered by
+                // iteration parity so one barrier suffices
+                int* fl = flags + (it & 1) * (kMlThreads / 64);
+                const unsigned long long wb = __ballot(bad != 0u);
+                if ((tid & 63) == 0) fl[tid >> 6] = wb != 0ull;
+                __syncthreads();
+                int any_bad = 0;
 #pragma unroll
-            for (int w = 0; w < kMlThreads / 64; ++w) any_bad |= fl[w];
-            if (it > 1 && !any_bad) {
-                conv = true;
-                break;
+                for (int w = 0; w < kMlThreads / 64; ++w) any_bad |= fl[w];
+                if (!any_bad) {
+                    conv = true;
+                    break;
+                }
+                if (!work) break;
             }
-            if (!work) break;
             // ---- C: variable pass.  Each edge's slot is read and rewritten by its
             // own variable only (c2v in, new v2c out), so no barrier separates them
             opaque_edges();
@@ -2007,7 +2051,9 @@ bool lds_kernel_applies(const DevGraph& g, int method, int precision, const Deco
         return g.opt_lds_kernel == 1 || block_placement(g, 8) != 3;
     }
     if (precision != 1) return false;
-    if (g.n > 16 * kMlThreads || g.m <= 0 || g.m > kMlNch * kMlThreads || ml_lds_bytes(g) > 160 * 1024) return false;
+    if (g.n > 16 * kMlThreads || g.m <= 0 || g.m > kMlNch * kMlThreads || a.max_iter < 1 ||
+        ml_lds_bytes(g) > 160 * 1024)
+        return false;
     if (block_placement(g, 4) == 0) return false;  // the SSF/finalize state would not fit LDS
     if (g.opt_lds_kernel == 0) return false;
     if (g.opt_lds_kernel == 1) return true;
@@ -2015,7 +2061,8 @@ bool lds_kernel_applies(const DevGraph& g, int method, int precision, const Deco
 }
 
 template <int VPT>
-static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream) {
+static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus, hipStream_t stream, float* img,
+                            size_t img_bytes) {
     const size_t lds = ml_lds_bytes(g);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bp_ms_lds_kernel<VPT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2024,13 +2071,19 @@ static int launch_lds_typed(const DevGraph& g, const DecodeArgs& a, int num_cus,
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_ms_lds_kernel<VPT>, kMlThreads, lds);
     if (e != hipSuccess) return (int)e;
     if (per_cu <= 0) return (int)hipErrorInvalidConfiguration;
+    if (!img || img_bytes < ml_image_bytes(g)) return (int)hipErrorInvalidValue;
     const long long grid = std::min<long long>((long long)num_cus * per_cu, a.B);
     e = hipMemsetAsync(a.wave_ctr, 0, sizeof(unsigned long long), stream);  // shot counter
     if (e != hipSuccess) return (int)e;
+    const float* prior = reinterpret_cast<const float*>(g.prior[1][1]);
+    hipLaunchKernelGGL(ml_init_scatter_kernel, dim3((unsigned)((g.n + 255) / 256)), dim3(256), 0, stream, g, g.ml_etab,
+                       prior, img);
+    hipLaunchKernelGGL(ml_init_check_kernel, dim3((unsigned)((g.m + 255) / 256)), dim3(256), 0, stream, g, img,
+                       a.ms_scaling);
     record_ev(a, 0, stream);
     QDEC_NOTE_BP("qdec::bp_ms_lds_kernel", VPT);
     hipLaunchKernelGGL((bp_ms_lds_kernel<VPT>), dim3((unsigned)grid), dim3(kMlThreads), lds, stream, g, a, g.ml_etab,
-                       reinterpret_cast<const float*>(g.prior[1][1]));
+                       prior, img);
     const hipError_t le = hipGetLastError();
     record_ev(a, 1, stream);
     if (le != hipSuccess) return (int)le;
@@ -2086,12 +2139,13 @@ static int launch_lds(const DevGraph& g, int precision, const DecodeArgs& a, int
         if (d3r >= 3) return launch_lds64_typed<10, 3>(g, a, num_cus, stream, img, scratch_bytes);
         return launch_lds64_typed<10, 0>(g, a, num_cus, stream, img, scratch_bytes);
     }
+    float* fimg = reinterpret_cast<float*>(scratch);  // f32: iteration 1's c2v rows
     const int vpt = (g.n + kMlThreads - 1) / kMlThreads;
-    if (vpt <= 4) return launch_lds_typed<4>(g, a, num_cus, stream);
-    if (vpt <= 8) return launch_lds_typed<8>(g, a, num_cus, stream);
-    if (vpt <= 10) return launch_lds_typed<10>(g, a, num_cus, stream);
-    if (vpt <= 12) return launch_lds_typed<12>(g, a, num_cus, stream);
-    return launch_lds_typed<16>(g, a, num_cus, stream);
+    if (vpt <= 4) return launch_lds_typed<4>(g, a, num_cus, stream, fimg, scratch_bytes);
+    if (vpt <= 8) return launch_lds_typed<8>(g, a, num_cus, stream, fimg, scratch_bytes);
+    if (vpt <= 10) return launch_lds_typed<10>(g, a, num_cus, stream, fimg, scratch_bytes);
+    if (vpt <= 12) return launch_lds_typed<12>(g, a, num_cus, stream, fimg, scratch_bytes);
+    return launch_lds_typed<16>(g, a, num_cus, stream, fimg, scratch_bytes);
 }
 
 // ---------------------------------------------------------------- slot-group launch
@@ -2220,8 +2274,9 @@ size_t block_scratch_bytes(const DevGraph& g, int method, int precision, int num
                                                                   : 0;
         return kGrpHeader + (size_t)group_count(g, method, tsz, num_cus, a.B) * group_layout(g, tsz).total + fin;
     }
-    // LDS-resident kernels: f64 takes iteration 1's state image (m64_init_kernel)
-    if (lds_kernel_applies(g, method, precision, a)) return precision == 0 ? m64_image_bytes(g) : 0;
+    // LDS-resident kernels: iteration 1's image (f64: check states, m64_init_kernel;
+    // f32: c2v rows, ml_init_*_kernel)
+    if (lds_kernel_applies(g, method, precision, a)) return precision == 0 ? m64_image_bytes(g) : ml_image_bytes(g);
     const int placement = block_placement(g, tsz);
     if (placement == 3) return 0;
     // shot-counter header + up to 4 workgroup slices per CU (+ the SSF/finalize
