@@ -232,6 +232,9 @@ def test_lds_kernel_random_irregular(gpu_available, oracle_lib, seed, monkeypatc
     probs = rng.uniform(0.005, 0.1, n)
     for scaling in (0.0, 0.625):
         _decode_both(oracle_lib, H, probs, syn, max_iter=30, ms_scaling=scaling)
+    # iteration 1 comes from the launch's image (no check pass): 1 and 2 iterations
+    for mi in (1, 2):
+        _decode_both(oracle_lib, H, probs, syn, max_iter=mi, ms_scaling=0.625 if mi == 2 else 0.0)
 
 
 def test_lds_kernel_zero_and_negative_priors(gpu_available, oracle_lib, monkeypatch):
