@@ -75,8 +75,10 @@ __device__ __forceinline__ int copy_bytes8(const uint8_t* src, uint8_t* dst, int
 // fold(xh), fail = any_r parity(lz[r] & (readout ^ corr)) (per-thread word parities
 // xor-reduced into LDS), status, ssf_steps.
 __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t shot, const uint8_t* xh, bool conv,
-                               bool satisfied, int steps, int* lpar /* LDS [k] */) {
+                               bool satisfied, int steps, int* lpar /* LDS [k] */,
+                               const uint8_t* rd_lds = nullptr /* LDS copy of the shot's readout, or null */) {
     const int tid = threadIdx.x;
+    auto rd = [&](int q) -> uint8_t { return rd_lds ? rd_lds[q] : a.readout[shot * g.n_data + q]; };
     if (a.x_out)
         for (int j = tid; j < g.n; j += kBlock) a.x_out[shot * g.n + j] = xh[j];
     const bool want_fail = a.fail && a.readout && g.k > 0;
@@ -95,7 +97,7 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int q = q0 + u * kBlock;
-                rv[u] = q < nd ? a.readout[shot * nd + q] : (uint8_t)0;
+                rv[u] = q < nd ? rd(q) : (uint8_t)0;
                 bv[u] = (q < nd && a.base) ? a.base[shot * nd + q] : (uint8_t)0;
             }
 #pragma unroll
@@ -118,7 +120,7 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
             int par = 0;
             for (int t = g.lz_ptr[r]; t < g.lz_ptr[r + 1]; ++t) {
                 const int q = g.lz_idx[t];
-                int cb = a.readout[shot * g.n_data + q] ^ (a.base ? a.base[shot * g.n_data + q] : 0);
+                int cb = rd(q) ^ (a.base ? a.base[shot * g.n_data + q] : 0);
                 for (int b = 0; b < g.fold_blocks; ++b) cb ^= xh[b * g.n_data + q];
                 par ^= cb & 1;
             }
@@ -148,7 +150,7 @@ __device__ void finalize_block(const DevGraph& g, const DecodeArgs& a, int64_t s
                 for (int u = 0; u < 8; ++u) {
                     const int q = (wbase + wv * 64 + i0 + u) * 64 + lane;
                     const bool in = q < g.n_data && wbase + wv * 64 + i0 + u < g.lz_words;
-                    rv[u] = in ? a.readout[shot * g.n_data + q] : (uint8_t)0;
+                    rv[u] = in ? rd(q) : (uint8_t)0;
                     bv[u] = (in && a.base) ? a.base[shot * g.n_data + q] : (uint8_t)0;
                 }
 #pragma unroll
@@ -593,7 +595,8 @@ __global__ __launch_bounds__(kBlock) void ssf_block_kernel(DevGraph g, DecodeArg
 __host__ __device__ inline size_t ssf_inc_lds(const DevGraph& g) {
     const size_t gp = (size_t)g.g_pad;
     return kCtrl + gp * 4 + gp * 4 + (gp * 2 + 15) / 16 * 16 + ((gp + 31) / 32 * 4 + 15) / 16 * 16 +
-           ((size_t)g.n_pad + 15) / 16 * 16 + ((size_t)g.m_pad + 15) / 16 * 16 + 4 * (size_t)(g.k > 0 ? g.k : 1);
+           ((size_t)g.n_pad + 15) / 16 * 16 + ((size_t)g.m_pad + 15) / 16 * 16 +
+           (4 * (size_t)(g.k > 0 ? g.k : 1) + 15) / 16 * 16 + ((size_t)g.n_data + 15) / 16 * 16;
 }
 
 __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, DecodeArgs a) {
@@ -609,8 +612,20 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
     uint8_t* xh = reinterpret_cast<uint8_t*>(dbits) + ((gp + 31) / 32 * 4 + 15) / 16 * 16;
     uint8_t* sres = xh + ((size_t)g.n_pad + 15) / 16 * 16;
     int* lpar = reinterpret_cast<int*>(sres + ((size_t)g.m_pad + 15) / 16 * 16);
-    const int tid = threadIdx.x, m = g.m, n = g.n, ng = g.n_gen;
+    uint8_t* rdl = reinterpret_cast<uint8_t*>(lpar) + (4 * (size_t)(g.k > 0 ? g.k : 1) + 15) / 16 * 16;
+    const int tid = threadIdx.x, m = g.m, n = g.n, ng = g.n_gen, nd = g.n_data;
     const int count = *a.q_count;
+    // whole rows by 16-B loads, every load of a shot issued before the first LDS
+    // store, when the rows allow (16-B multiples at 16-B aligned bases, <= kRowU
+    // loads per thread): the byte rounds of copy_bytes8 (8 bytes of a thread's
+    // share per HBM round trip) made the rows' loads ~8 dependent round trips
+    // per shot at n = 10^4.  The readout row goes to LDS too (finalize_block).
+    constexpr int kRowU = 3;
+    const bool want_rd = a.fail && a.readout && g.k > 0;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool vec = ((n | m | (want_rd ? nd : 0)) & 15) == 0 && al16(a.q_x) && al16(a.q_r) &&
+                     (!want_rd || al16(a.readout)) && n <= 16 * kRowU * kBlock && m <= 16 * kRowU * kBlock &&
+                     nd <= 16 * kRowU * kBlock;
     const int nhi = g.g_wmax > 4 ? (1 << (g.g_wmax - 4)) : 1;
     for (int w = tid; w < (int)((gp + 31) / 32); w += kBlock) dbits[w] = 0u;
     if (tid == 0) ctl[0] = 0;
@@ -641,8 +656,33 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
         // the queued hard decision and residual, eight loads in flight per
         // thread before any LDS store (a loop of single byte loads waited for
         // each one: ~40 HBM round trips per shot at n = 10^4)
-        copy_bytes8(a.q_x + (int64_t)slot * n, xh, n, tid);
-        int wl = copy_bytes8(a.q_r + (int64_t)slot * m, sres, m, tid);
+        int wl = 0;
+        if (vec) {
+            uint4 vx[kRowU], vr[kRowU], vd[kRowU];
+            const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int u = 0; u < kRowU; ++u) {
+                const int j = (u * kBlock + tid) * 16;
+                vx[u] = j < n ? *reinterpret_cast<const uint4*>(a.q_x + (int64_t)slot * n + j) : z;
+                vr[u] = j < m ? *reinterpret_cast<const uint4*>(a.q_r + (int64_t)slot * m + j) : z;
+                vd[u] = (want_rd && j < nd) ? *reinterpret_cast<const uint4*>(a.readout + shot * nd + j) : z;
+            }
+#pragma unroll
+            for (int u = 0; u < kRowU; ++u) {
+                const int j = (u * kBlock + tid) * 16;
+                if (j < n) *reinterpret_cast<uint4*>(xh + j) = vx[u];
+                if (j < m) {
+                    *reinterpret_cast<uint4*>(sres + j) = vr[u];
+                    // bytes are 0 / 1: the bit count is the byte sum
+                    wl += __builtin_popcount(vr[u].x) + __builtin_popcount(vr[u].y) + __builtin_popcount(vr[u].z) +
+                          __builtin_popcount(vr[u].w);
+                }
+                if (want_rd && j < nd) *reinterpret_cast<uint4*>(rdl + j) = vd[u];
+            }
+        } else {
+            copy_bytes8(a.q_x + (int64_t)slot * n, xh, n, tid);
+            wl = copy_bytes8(a.q_r + (int64_t)slot * m, sres, m, tid);
+        }
         int sw = block_sum_i32(wl, redi);  // includes a barrier: LDS fills visible
         int steps = 0;
         if (a.ssf && sw > 0) {
@@ -728,7 +768,7 @@ __global__ __launch_bounds__(kBlock) void ssf_inc_block_kernel(DevGraph g, Decod
                 ++steps;
             }
         }
-        finalize_block(g, a, shot, xh, bp_conv, sw == 0, steps, lpar);
+        finalize_block(g, a, shot, xh, bp_conv, sw == 0, steps, lpar, vec && want_rd ? rdl : nullptr);
     }
 }
 
